@@ -1,0 +1,44 @@
+# Build for the MI355X-native path tracer (gfx950) and its CPU oracle.
+#   make            -> librtx.so + rtx_cli + liboracle.so (+ oracle/_ref when /root/reference exists)
+# -ffp-contract=off everywhere: fused multiply-adds only where written as fmaf,
+# so the HIP kernel and the C oracle execute the same IEEE op sequence.
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+PKG       := raytrace-we-gpu_amd
+SRC       := $(PKG)/csrc
+LIBDIR    := $(PKG)/lib
+BINDIR    := $(PKG)/bin
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+LIB       := $(LIBDIR)/librtx.so
+CLI       := $(BINDIR)/rtx_cli
+HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h
+
+all: $(LIB) $(CLI) oracle
+
+$(LIBDIR)/%.o: $(SRC)/%.hip $(HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/rtx_host.o: $(SRC)/rtx_host.cpp include/rtx.h | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/rtx_kernels.o $(LIBDIR)/rtx_api.o $(LIBDIR)/rtx_host.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+
+$(CLI): $(SRC)/rtx_cli.cpp $(SRC)/rtx_app.cpp include/rtx.h include/rtx_app.hpp $(LIB) | $(BINDIR)
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Wall -o $@ $(SRC)/rtx_cli.cpp $(SRC)/rtx_app.cpp \
+	    -L$(LIBDIR) -lrtx -Wl,-rpath,'$$ORIGIN/../lib' -lpthread
+
+$(LIBDIR) $(BINDIR):
+	mkdir -p $@
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $(SRC)/rtx_kernels.hip -o $(LIBDIR)/rtx_kernels.s
+
+clean:
+	rm -rf $(LIBDIR) $(BINDIR)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle asm clean

@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the MI355X path tracer on BASELINE.json's config.
+
+Workload (BASELINE.json configs[1]): 1920x1080, RTIOW final
+random-sphere scene (WorldDef::random_world with grid -11..11 = 486
+spheres), spp 100, depth 50, the reference's chain RNG. One step = one
+frame: every rank renders its interleaved row tiles (rtx_render_rows), the
+ranks gather to rank 0 over RCCL (torch.distributed "nccl" = RCCL) and
+rank 0 de-interleaves into the image. Scene/camera are resident on the
+device before timing. Launch:
+
+    python bench.py [--gpus 1] [--steps 10] [--warmup 2]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line. `value` = pixels*spp*steps / max-over-ranks
+wall time of the timed steps: the frame is split across ranks, so the work
+per step is fixed as N grows ("scaling": "strong").
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytrace-we-gpu_amd"))
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FLOP_PER_TEST = 20        # algorithmic FLOP per ray-sphere test
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=100)
+    p.add_argument("--depth", type=int, default=50)
+    p.add_argument("--grid", type=int, default=11, help="random_world grid half extent (11 -> 486 spheres)")
+    p.add_argument("--max-spheres", type=int, default=0)
+    p.add_argument("--tile-rows", type=int, default=5)
+    p.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                   help="rocprofv3 PMC child passes for HBM traffic (rank 0, N=1)")
+    p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+def scene_and_frame(args):
+    import rtx
+    cap = args.max_spheres or None
+    world = rtx.random_world(args.grid, capacity=cap, depth=args.depth, spp=args.spp)
+    frame = rtx.camera_look_at(args.width, args.height, aspect=args.width / args.height)
+    frame.rng_mode = 1 if args.rng == "per-sample" else 0
+    return world, frame
+
+
+def probe(args):
+    """One frame through the C-ABI, no torch: the process rocprofv3 wraps."""
+    import rtx
+    world, frame = scene_and_frame(args)
+    with rtx.Context(0) as ctx:
+        ctx.upload_world(world)
+        ctx.set_frame(frame)
+        ctx.render()
+        ctx.sync()
+
+
+def pmc_traffic(args):
+    """HBM bytes per render launch from rocprofv3 PMC counters, per
+    MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes
+    (TCC slots), KB units, FETCH_SIZE x2 on gfx950 for wide coalesced reads.
+    Returns (bytes, details) or (None, reason)."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    vals = {}
+    base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
+            "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
+            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", args.rng]
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="rtx_pmc_")
+        cmd = [exe, "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=240)
+        except Exception as e:  # noqa: BLE001
+            return None, f"rocprofv3 {ctr} failed: {type(e).__name__}"
+        total, n = 0.0, 0
+        for path in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
+            for row in csv.DictReader(open(path)):
+                if "k_render" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    total += float(row["Counter_Value"])
+                    n += 1
+        shutil.rmtree(out, ignore_errors=True)
+        if n == 0:
+            return None, f"no {ctr} rows for k_render"
+        vals[ctr] = total
+    kb = 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]
+    return kb * 1024.0, {"FETCH_SIZE_KB": vals["FETCH_SIZE"], "WRITE_SIZE_KB": vals["WRITE_SIZE"],
+                         "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+
+
+def cpu_baseline(args, world, frame, gpu_image, budget_s):
+    """The fp32 oracle (port of the reference path) on the host cores, on a
+    bounded sample of the same frame: whole rows at full spp, spread over
+    the image, until the time budget is spent. Those rows are also compared
+    bit for bit with the GPU frame."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    H = args.height
+    order = [(7 + 37 * k) % H for k in range(H)]  # 37 is coprime to 1080: every row once
+    done, t0, mism = [], time.perf_counter(), 0
+    while done == [] or (time.perf_counter() - t0 < budget_s and len(done) < H):
+        batch = order[len(done):len(done) + threads]
+        if not batch:
+            break
+        rows, _ = oracle.render_rows(world, frame, np.array(batch, np.uint32), nthreads=threads)
+        if gpu_image is not None:
+            g = gpu_image[batch]
+            same = (g.view(np.uint32) == rows.view(np.uint32)) | (np.isnan(g) & np.isnan(rows))
+            mism += int((~same).sum())
+        done += batch
+    dt = time.perf_counter() - t0
+    samples = len(done) * args.width * args.spp
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{len(done)} full rows (x{args.width} px, spp {args.spp}) of the same frame, "
+                      f"spread over the image, fp32 oracle (oracle/rtx_oracle.c), {threads} threads, "
+                      f"{dt:.1f} s"}, {"rows_checked": len(done), "values_differing": mism,
+                                       "bit_exact": mism == 0}
+
+
+def main():
+    args = parse()
+    if args.probe:
+        probe(args)
+        return
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import rtx
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        if world_size == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        args.gpus = world_size
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    world, frame = scene_and_frame(args)
+    W, H, T, R = args.width, args.height, args.tile_rows, world_size
+    stream = torch.cuda.current_stream()
+    ctx = rtx.Context(local_rank, stream=stream.cuda_stream)
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    max_rows = rtx.part_rows(H, T, 0, R)
+    dev = torch.device("cuda", local_rank)
+    image = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+    if R > 1:
+        send = torch.empty((max_rows, W, 4), dtype=torch.float32, device=dev)
+        gathered = torch.empty((R, max_rows, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        gather_list = list(gathered.unbind(0)) if rank == 0 else None
+
+    def step():
+        if R == 1:
+            ctx.render_rows(1, 0, 1, image.data_ptr())
+            return
+        ctx.render_rows(T, rank, R, send.data_ptr())
+        dist.gather(send, gather_list=gather_list, dst=0)
+        if rank == 0:
+            ctx.deinterleave(gathered.data_ptr(), W, H, T, R, image.data_ptr())
+
+    def barrier():
+        if R > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.stats_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if R > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = ctx.stats()
+
+    if rank == 0:
+        samples = W * H * args.spp * args.steps
+        value = samples / elapsed / 1e6
+        launch_ms = st.kernel_ms / max(1, st.launches)
+        tests_per_launch = st.sphere_tests / max(1, st.launches)
+        flops = FLOP_PER_TEST * tests_per_launch
+        achieved = flops / (launch_ms * 1e-3) / 1e12
+        rows0 = rtx.part_rows(H, T, 0, R) if R > 1 else H
+        alg_bytes = rows0 * W * 16 + world.count * 32  # framebuffer + scene
+        traffic, pmc_note = (None, "skipped")
+        if args.pmc == "auto" and R == 1:
+            traffic, pmc_note = pmc_traffic(args)
+        host_img = image.cpu().numpy() if R == 1 else None
+        cpu, parity = (None, None)
+        if R == 1 and args.cpu_seconds > 0:
+            cpu, parity = cpu_baseline(args, world, frame, host_img, args.cpu_seconds)
+        line = {
+            "metric": "Msamples/sec (pixels x spp) at 1920x1080 spp=100 depth=50",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": R,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic RTIOW random_world scene, MSVC-rand LCG)",
+            "config": {"workload": f"RTIOW final scene {W}x{H}, spp {args.spp}, depth {args.depth}, "
+                                   f"{world.count} spheres, {args.rng} RNG",
+                       "width": W, "height": H, "spp": args.spp, "depth": args.depth,
+                       "spheres": world.count, "rng": args.rng, "tile_rows": T,
+                       "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if R > 1 else "")},
+            "roofline": {"bound": "mfma", "roof": "fp32 vector ALU (157.3 TF = fp32 MFMA peak)",
+                         "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "kernel": "k_render_resident" if world.count <= 4096 else "k_render_streamed",
+                         "kernel_ms": round(launch_ms, 4),
+                         "flop_per_launch": flops, "sphere_tests_per_launch": tests_per_launch,
+                         "segments_per_sample": round(st.segments / max(1, st.samples), 4),
+                         "pmc": pmc_note},
+            "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(alg_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
+                             "algorithmic_bytes_per_launch": alg_bytes,
+                             "traffic": None if traffic is None else round(traffic)},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if R > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

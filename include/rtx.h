@@ -1,0 +1,220 @@
+/*
+ * rtx.h — C-ABI of the MI355X-native sphere path tracer (librtx.so).
+ *
+ * This is the drop-in boundary for the reference's GPU path. In
+ * Brochu/RayTrace-WE-GPU the host app (CSVersion/DxCSApp.cpp) talks to the
+ * GPU through D3D11 objects owned by CDx11Base (CSVersion/Dx11Base.h:11-40):
+ *   - cbuffer b1 `WorldDef`   (DxCSApp.cpp:64-71, ShaderCompute.hlsl:12-19),
+ *     IMMUTABLE, uploaded once in LoadContent (DxCSApp.cpp:393-413);
+ *   - cbuffer b0 `PerFrame`   (DxCSApp.cpp:30-37, ShaderCompute.hlsl:3-10),
+ *     DYNAMIC, Map/memcpy/Unmap every Update (DxCSApp.cpp:481-496);
+ *   - UAV slot 0 RWTexture2D<float4> (DxCSApp.cpp:326-356, :519) written by
+ *     `CSMain` (ShaderCompute.hlsl:291-315);
+ *   - Dispatch(32,32,1) (DxCSApp.cpp:524).
+ * Every entry point below names the reference call it replaces.
+ *
+ * Conventions: plain C types only; no exceptions cross the ABI; every
+ * function returns RTX_OK (0) or a negative RTX_ERR_* code and then
+ * rtx_last_error() (thread-local) describes the failure. A context is bound
+ * to one HIP device and is not thread-safe (the reference drives one D3D11
+ * immediate context from the UI thread). Framebuffers are linear
+ * float4[rows * width], row 0 = image bottom (the reference's DTid.y,
+ * ShaderCompute.hlsl:306-307 with the display quad's texcoords,
+ * DxCSApp.cpp:297-303).
+ */
+#ifndef RTX_H_
+#define RTX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define RTX_API __attribute__((visibility("default")))
+#else
+#define RTX_API
+#endif
+
+#define RTX_VERSION 100 /* 1.0.0 */
+
+enum {
+    RTX_OK = 0,
+    RTX_ERR_INVALID = -1, /* bad argument (null pointer, size mismatch, ...) */
+    RTX_ERR_HIP = -2,     /* a HIP runtime call failed */
+    RTX_ERR_STATE = -3,   /* call out of order (no world / no frame yet) */
+    RTX_ERR_NOMEM = -4    /* host or device allocation failed */
+};
+
+/* Material type codes, as the reference stores them in WorldDef::matTypes
+ * (DxCSApp.cpp:11-17 SetFloat4Cmpt; ShaderCompute.hlsl:209,219,229). */
+enum { RTX_MAT_LAMBERT = 0, RTX_MAT_METAL = 1, RTX_MAT_DIELECTRIC = 2 };
+
+/* RNG modes. CHAIN is the reference: ONE fp32 seed per pixel carried through
+ * all samples (ShaderCompute.hlsl:295, 304-309). PER_SAMPLE re-seeds every
+ * (pixel, sample) so samples are independent of each other (needed to split
+ * one pixel's samples across lanes/GPUs); it is an extension, not reference
+ * behaviour. */
+enum { RTX_RNG_CHAIN = 0, RTX_RNG_PER_SAMPLE = 1 };
+
+/* Scene (~ cbuffer b1 WorldDef, DxCSApp.cpp:64-71). Arrays are read during
+ * rtx_upload_world and copied; the caller keeps ownership. Unlike the
+ * reference's fixed 512-sphere cbuffer the count is unbounded. */
+typedef struct rtx_world {
+    uint32_t count;           /* sceneValues.x : number of spheres           */
+    uint32_t depth;           /* sceneValues.y : max ray segments per sample */
+    uint32_t spp;             /* sceneValues.z : samples per pixel           */
+    uint32_t reserved;        /* must be 0                                   */
+    const float *spheres;     /* 4*count : center.xyz, radius  (spheres[])   */
+    const float *mat_types;   /* count   : RTX_MAT_* as float  (matTypes[])  */
+    const float *mat_values;  /* 4*count : albedo.rgb, fuzz-or-ir (matValues[]) */
+} rtx_world;
+
+/* Per-frame constants (~ cbuffer b0 PerFrame, DxCSApp.cpp:30-37). The four
+ * rows are the reference's viewVals as the shader reads them
+ * (ShaderCompute.hlsl:122-123): origin, horizontal, vertical, lower-left. */
+typedef struct rtx_frame {
+    float origin[4];          /* viewVals[0] */
+    float horizontal[4];      /* viewVals[1] */
+    float vertical[4];        /* viewVals[2] */
+    float lower_left[4];      /* viewVals[3] */
+    float img_w;              /* img_dim.x = perspectiveVals.w               (ShaderCompute.hlsl:294) */
+    float img_h;              /* img_dim.y = perspectiveVals.w / perspectiveVals.y */
+    uint32_t width;           /* framebuffer width in pixels  (texture Width,  DxCSApp.cpp:331) */
+    uint32_t height;          /* framebuffer height in pixels (texture Height, DxCSApp.cpp:330) */
+    uint32_t rng_mode;        /* RTX_RNG_*; 0 = reference                     */
+    uint32_t frame_index;     /* seed offset for progressive frames; 0 = reference (time unused, :296) */
+    uint32_t reserved[2];     /* must be 0 */
+} rtx_frame;
+
+/* Counters of the last launches since rtx_stats_reset (measurement, §8d). */
+typedef struct rtx_stats {
+    double kernel_ms;         /* summed HIP-event duration of the render kernels */
+    uint64_t launches;        /* render kernel launches                          */
+    uint64_t samples;         /* pixel-samples traced (pixels * spp)             */
+    uint64_t segments;        /* hit_world calls (ray segments)                  */
+    uint64_t sphere_tests;    /* segments * sphere count (ray-sphere tests)      */
+} rtx_stats;
+
+typedef struct rtx_ctx rtx_ctx;
+
+/* ---- library / device ------------------------------------------------- */
+RTX_API int rtx_version(void);
+/* Thread-local text of the last failure on this thread ("" if none). */
+RTX_API const char *rtx_last_error(void);
+/* Number of visible HIP devices. */
+RTX_API int rtx_device_count(int *count);
+
+/* ---- context lifecycle (~ CDx11Base::Initialize / Terminate) ------------
+ * rtx_create replaces D3D11CreateDeviceAndSwapChain (CSVersion/Dx11Base.cpp:75)
+ * + the resource creation in LoadContent; rtx_destroy replaces
+ * CDx11Base::Terminate -> DxCSApp::UnloadContent (Dx11Base.cpp:134-152,
+ * DxCSApp.cpp:420-456). */
+RTX_API int rtx_create(int hip_device, rtx_ctx **out);
+RTX_API void rtx_destroy(rtx_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch's current stream) for every later
+ * launch; NULL restores the context's own stream. */
+RTX_API int rtx_set_stream(rtx_ctx *ctx, void *hip_stream);
+
+/* ---- scene / frame upload ----------------------------------------------
+ * ~ CreateBuffer(WorldDef, IMMUTABLE) (DxCSApp.cpp:393-413). */
+RTX_API int rtx_upload_world(rtx_ctx *ctx, const rtx_world *world);
+/* ~ Map(WRITE_DISCARD)/memcpy/Unmap of PerFrame (DxCSApp.cpp:494-496).
+ * Host-side only: constants travel as kernel arguments. */
+RTX_API int rtx_set_frame(rtx_ctx *ctx, const rtx_frame *frame);
+
+/* ---- render (~ Dispatch(32,32,1), DxCSApp.cpp:524) ------------------------
+ * Renders the rows owned by partition `part` of `nparts`: image rows are
+ * cut into tiles of `tile_rows` rows and tile k belongs to part k % nparts
+ * (interleaved row tiles). The part's rows are written in
+ * ascending order, contiguously, to d_out (device pointer, at least
+ * rtx_part_rows(...) * width float4s). d_out == NULL renders into the
+ * context's own framebuffer (whole image only: part 0 of 1).
+ * Asynchronous on the context stream. */
+RTX_API int rtx_render_rows(rtx_ctx *ctx, uint32_t tile_rows, uint32_t part,
+                            uint32_t nparts, void *d_out);
+/* Whole frame into the context framebuffer (= rtx_render_rows(ctx,1,0,1,NULL)). */
+RTX_API int rtx_render(rtx_ctx *ctx);
+/* Rows owned by `part` (host arithmetic, no GPU). */
+RTX_API uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part,
+                               uint32_t nparts);
+/* Gathered buffer [nparts][max_rows][width] (each part's rows, padded to
+ * the largest part) -> image [height][width] in global row order. Device
+ * pointers; asynchronous on the context stream. */
+RTX_API int rtx_deinterleave_rows(rtx_ctx *ctx, const void *d_gathered,
+                                  uint32_t width, uint32_t height,
+                                  uint32_t tile_rows, uint32_t nparts,
+                                  void *d_image);
+/* Wait for all work on the context stream (~ the implicit sync of Present,
+ * DxCSApp.cpp:551). */
+RTX_API int rtx_sync(rtx_ctx *ctx);
+/* Device pointer of the context framebuffer (width*height float4) or NULL. */
+RTX_API void *rtx_framebuffer(rtx_ctx *ctx);
+/* Copy the context framebuffer to host memory (synchronous). The reference
+ * never reads results back; this is the image-output contract (§8f-1). */
+RTX_API int rtx_download(rtx_ctx *ctx, float *host_rgba, size_t bytes);
+
+/* ---- measurement ------------------------------------------------------ */
+RTX_API int rtx_stats_reset(rtx_ctx *ctx);
+/* Synchronises the stream, then reports counters since the last reset. */
+RTX_API int rtx_get_stats(rtx_ctx *ctx, rtx_stats *out);
+
+/* ---- host-side producers (no GPU) ----------------------------------------
+ * WorldDef::random_world (DxCSApp.cpp:72-134) with MSVC rand() (unseeded,
+ * DxCSApp.cpp:6-9) emulated bit-exactly. grid_half_extent 9 = reference
+ * (326 spheres), 11 = RTIOW final scene (486). At most `capacity` spheres
+ * are written (the generator stops there); *count receives the number
+ * written. Arrays: spheres 4*capacity, mat_types capacity, mat_values
+ * 4*capacity. */
+RTX_API int rtx_scene_random_world(int32_t grid_half_extent, uint32_t capacity,
+                                   float *spheres, float *mat_types,
+                                   float *mat_values, uint32_t *count);
+/* WorldDef::test_world (DxCSApp.cpp:136-157): 4 spheres. */
+RTX_API int rtx_scene_test_world(float *spheres, float *mat_types,
+                                 float *mat_values, uint32_t *count);
+/* PerFrame::ComputeViewVals (DxCSApp.cpp:39-61) + the focus distance of
+ * DxCSApp::Update (DxCSApp.cpp:488) with focus_dist <= 0 meaning
+ * |from - at|. Fills the four view rows, img_w = width_px,
+ * img_h = width_px / aspect (ShaderCompute.hlsl:294) and width/height. */
+RTX_API int rtx_camera_look_at(const float from[3], const float at[3],
+                               const float vup[3], float vfov_deg, float aspect,
+                               float aperture, float focus_dist,
+                               uint32_t width_px, uint32_t height_px,
+                               rtx_frame *out);
+/* Camera(width, height) of the CPU library (Camera.h:9-21). */
+RTX_API int rtx_camera_simple(uint32_t width_px, uint32_t height_px, rtx_frame *out);
+/* Adapters from the reference's exact cbuffer byte layouts: WorldDef
+ * (18,448 B, DxCSApp.cpp:64-71) and PerFrame (112 B, DxCSApp.cpp:30-37,
+ * viewVals stored transposed, :60). The world adapter writes into
+ * caller arrays of capacity 512 like rtx_scene_random_world. */
+RTX_API int rtx_world_from_worlddef(const void *worlddef_bytes, size_t nbytes,
+                                    float *spheres, float *mat_types,
+                                    float *mat_values, rtx_world *out);
+RTX_API int rtx_frame_from_perframe(const void *perframe_bytes, size_t nbytes,
+                                    uint32_t width_px, uint32_t height_px,
+                                    rtx_frame *out);
+
+/* ---- debug entry points: the hot-path building blocks run on the GPU ----
+ * (used by the parity tests; same device code as the render kernel).
+ * rays: nrays * 6 floats (origin.xyz, dir.xyz) host memory. out: nrays * 10
+ * floats: hit(0/1), t, p.xyz, normal.xyz, front_face(0/1), sphere index.
+ * Uses the uploaded world. Synchronous. ~ hit_world, ShaderCompute.hlsl:188-205. */
+RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
+                                float t_min, float t_max, float *out);
+/* Evaluates device math function `fn` (RTX_FN_*) elementwise on host
+ * arrays (in0, in1 may be unused); out receives n floats (hash functions
+ * write 1, 2 or 3 floats per element: out must hold 3*n). Synchronous. */
+enum {
+    RTX_FN_SQRT = 0, RTX_FN_DIV = 1, RTX_FN_SIN = 2, RTX_FN_COS = 3,
+    RTX_FN_LOG2 = 4, RTX_FN_EXP2 = 5, RTX_FN_POW = 6, RTX_FN_BASEHASH = 7,
+    RTX_FN_HASH1 = 8, RTX_FN_HASH2 = 9, RTX_FN_HASH3 = 10, RTX_FN_RIUS = 11
+};
+RTX_API int rtx_debug_math(rtx_ctx *ctx, int fn, const float *in0,
+                           const float *in1, uint32_t n, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_H_ */

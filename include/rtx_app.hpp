@@ -1,0 +1,96 @@
+// rtx_app.hpp — C++ host surface mirroring the reference's app plug-in
+// interface, driven through the rtx C-ABI instead of D3D11.
+//
+//   RtxBase   ~ CDx11Base (CSVersion/Dx11Base.h:11-40): Initialize /
+//               Terminate + pure virtual LoadContent / UnloadContent /
+//               Update / Render.
+//   RtxCSApp  ~ DxCSApp  (CSVersion/DxCSApp.h:12-60, DxCSApp.cpp:160-552):
+//               LoadContent builds WorldDef::random_world and uploads it
+//               (DxCSApp.cpp:199-418); Update computes PerFrame's camera
+//               (:458-497); Render launches the path tracer (:499-552).
+// Errors: bool returns like the reference (false + rtx_last_error()).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rtx.h"
+
+namespace rtx {
+
+class RtxBase {
+public:
+    RtxBase() = default;
+    virtual ~RtxBase();
+    RtxBase(const RtxBase &) = delete;
+    RtxBase &operator=(const RtxBase &) = delete;
+
+    // ~ CDx11Base::Initialize(HWND, HINSTANCE) (CSVersion/Dx11Base.cpp:23-132):
+    // creates the device context, then calls LoadContent.
+    bool Initialize(int hip_device);
+    // ~ CDx11Base::Terminate (CSVersion/Dx11Base.cpp:134-152).
+    void Terminate();
+
+    virtual bool LoadContent() = 0;
+    virtual void UnloadContent() = 0;
+    virtual void Update() = 0;
+    virtual void Render() = 0;
+
+    rtx_ctx *context() const { return m_ctx; }
+    const std::string &last_error() const { return m_error; }
+
+protected:
+    rtx_ctx *m_ctx = nullptr;
+    std::string m_error;
+};
+
+enum class SceneKind { RandomWorld, TestWorld };
+
+struct AppConfig {
+    uint32_t width = 1024, height = 576;   // texture size, DxCSApp.cpp:330-331
+    uint32_t spp = 60, depth = 50;         // sceneValues, DxCSApp.cpp:133
+    SceneKind scene = SceneKind::RandomWorld;
+    int32_t grid_half_extent = 9;          // random_world grid, DxCSApp.cpp:95-97
+    uint32_t max_spheres = 0;              // 0 = no cap
+    float cam_pos[3] = {13.0f, 2.0f, 3.0f};   // DxCSApp.cpp:176
+    float cam_look_at[3] = {0.0f, 0.0f, 0.0f};
+    float up[3] = {0.0f, 1.0f, 0.0f};
+    float vfov = 20.0f;                    // perspectiveVals, DxCSApp.cpp:179
+    float aspect = 16.0f / 9.0f;
+    float aperture = 2.0f;
+    bool simple_camera = false;            // Camera.h instead of ComputeViewVals
+    uint32_t rng_mode = RTX_RNG_CHAIN;
+};
+
+class RtxCSApp : public RtxBase {
+public:
+    explicit RtxCSApp(const AppConfig &cfg = AppConfig());
+    ~RtxCSApp() override;
+
+    bool LoadContent() override;
+    void UnloadContent() override;
+    void Update() override;
+    void Render() override;
+
+    // Image output contract (§8f-1): the framebuffer, row 0 = image bottom.
+    bool Download(std::vector<float> &rgba);
+    const AppConfig &config() const { return m_cfg; }
+    uint32_t sphere_count() const { return m_count; }
+    bool ok() const { return m_ok; }
+
+private:
+    AppConfig m_cfg;
+    std::vector<float> m_spheres, m_mat_types, m_mat_values;
+    uint32_t m_count = 0;
+    rtx_frame m_frame{};
+    uint32_t m_frame_count = 0;  // ~ sampleCount, DxCSApp.cpp:491
+    bool m_ok = true;
+};
+
+// PFM (float RGB, rows stored bottom-to-top = our row order) and binary
+// PPM (8-bit, top-to-bottom: rows flipped, values clamped to [0,1]).
+bool write_pfm(const std::string &path, const float *rgba, uint32_t w, uint32_t h);
+bool write_ppm(const std::string &path, const float *rgba, uint32_t w, uint32_t h);
+
+}  // namespace rtx

@@ -1,0 +1,425 @@
+// rtx_api.hip — C-ABI context management for librtx.so (include/rtx.h).
+//
+// Replaces the D3D11 objects the reference's DxCSApp owns
+// (CSVersion/DxCSApp.h:33-59): the IMMUTABLE WorldDef cbuffer becomes
+// device arrays (rtx_upload_world), the DYNAMIC PerFrame cbuffer becomes
+// kernel arguments (rtx_set_frame), the RWTexture2D UAV becomes a linear
+// float4 framebuffer, Dispatch becomes rtx_render_rows.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rtx.h"
+#include "rtx_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(RTX_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RTX_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+struct EventPair {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
+}  // namespace
+
+struct rtx_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;  // own_stream or an external one
+    // scene (device)
+    float4 *d_sph = nullptr;
+    float *d_rad = nullptr;
+    int *d_mtype = nullptr;
+    float4 *d_mval = nullptr;
+    uint32_t n = 0, n_pad = 0, depth = 0, spp = 0;
+    bool have_world = false;
+    // frame
+    rtx_frame frame{};
+    bool have_frame = false;
+    // framebuffer
+    float4 *d_fb = nullptr;
+    size_t fb_pixels = 0;
+    // measurement
+    unsigned long long *d_counters = nullptr;
+    std::vector<EventPair> events;  // one pair per launch since reset
+    size_t events_used = 0;
+    uint64_t samples = 0;
+    uint64_t launches = 0;
+    bool n_changed = false;  // world resized since the last rtx_stats_reset
+};
+
+namespace {
+
+int set_device(rtx_ctx *c) {
+    RTX_HIP(hipSetDevice(c->device));
+    return RTX_OK;
+}
+
+void free_world(rtx_ctx *c) {
+    (void)hipFree(c->d_sph);
+    (void)hipFree(c->d_rad);
+    (void)hipFree(c->d_mtype);
+    (void)hipFree(c->d_mval);
+    c->d_sph = nullptr;
+    c->d_rad = nullptr;
+    c->d_mtype = nullptr;
+    c->d_mval = nullptr;
+    c->have_world = false;
+}
+
+rtx::KScene scene_of(const rtx_ctx *c) {
+    rtx::KScene s;
+    s.sph = c->d_sph;
+    s.rad = c->d_rad;
+    s.mtype = c->d_mtype;
+    s.mval = c->d_mval;
+    s.n = c->n;
+    s.n_pad = c->n_pad;
+    return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtx_version(void) { return RTX_VERSION; }
+
+const char *rtx_last_error(void) { return g_last_error.c_str(); }
+
+int rtx_device_count(int *count) {
+    if (!count) return fail(RTX_ERR_INVALID, "rtx_device_count: null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return hip_fail(e, "hipGetDeviceCount");
+    }
+    *count = n;
+    return RTX_OK;
+}
+
+int rtx_create(int hip_device, rtx_ctx **out) {
+    if (!out) return fail(RTX_ERR_INVALID, "rtx_create: null out");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    if (hip_device < 0 || hip_device >= ndev)
+        return fail(RTX_ERR_INVALID, "rtx_create: device " + std::to_string(hip_device) +
+                                         " out of range (" + std::to_string(ndev) + " devices)");
+    rtx_ctx *c = new (std::nothrow) rtx_ctx();
+    if (!c) return fail(RTX_ERR_NOMEM, "rtx_create: out of host memory");
+    c->device = hip_device;
+    int rc = set_device(c);
+    if (rc != RTX_OK) {
+        delete c;
+        return rc;
+    }
+    e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    c->stream = c->own_stream;
+    e = hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return hip_fail(e, "hipMalloc(counters)");
+    }
+    *out = c;
+    return RTX_OK;
+}
+
+void rtx_destroy(rtx_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_world(c);
+    (void)hipFree(c->d_fb);
+    (void)hipFree(c->d_counters);
+    for (auto &p : c->events) {
+        (void)hipEventDestroy(p.start);
+        (void)hipEventDestroy(p.stop);
+    }
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int rtx_set_stream(rtx_ctx *c, void *s) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_set_stream: null ctx");
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    return RTX_OK;
+}
+
+int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
+    if (!c || !w) return fail(RTX_ERR_INVALID, "rtx_upload_world: null argument");
+    if (w->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_upload_world: reserved must be 0");
+    if (w->count > 0 && (!w->spheres || !w->mat_types || !w->mat_values))
+        return fail(RTX_ERR_INVALID, "rtx_upload_world: null array with count > 0");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const uint32_t n = w->count;
+    const uint32_t n_pad = (n + rtx::kPad - 1) / rtx::kPad * rtx::kPad;
+    std::vector<float4> sph(n_pad), mval(n);
+    std::vector<float> rad(n);
+    std::vector<int> mtype(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float r = w->spheres[4 * i + 3];
+        sph[i] = make_float4(w->spheres[4 * i + 0], w->spheres[4 * i + 1], w->spheres[4 * i + 2],
+                             -(r * r));
+        rad[i] = r;
+        // The shader compares the float code with 0, 1, 2 (:209,219,229);
+        // anything else does not scatter.
+        const float t = w->mat_types[i];
+        mtype[i] = (t == 0.0f) ? 0 : (t == 1.0f) ? 1 : (t == 2.0f) ? 2 : 3;
+        mval[i] = make_float4(w->mat_values[4 * i + 0], w->mat_values[4 * i + 1],
+                              w->mat_values[4 * i + 2], w->mat_values[4 * i + 3]);
+    }
+    for (uint32_t i = n; i < n_pad; ++i) sph[i] = sph[n - 1];  // see rtx::KScene
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    free_world(c);
+    const size_t cap = n ? n : 1;
+    RTX_HIP(hipMalloc(&c->d_sph, (n_pad ? n_pad : 1) * sizeof(float4)));
+    RTX_HIP(hipMalloc(&c->d_rad, cap * sizeof(float)));
+    RTX_HIP(hipMalloc(&c->d_mtype, cap * sizeof(int)));
+    RTX_HIP(hipMalloc(&c->d_mval, cap * sizeof(float4)));
+    if (n) {
+        RTX_HIP(hipMemcpy(c->d_sph, sph.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice));
+        RTX_HIP(hipMemcpy(c->d_rad, rad.data(), n * sizeof(float), hipMemcpyHostToDevice));
+        RTX_HIP(hipMemcpy(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice));
+        RTX_HIP(hipMemcpy(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    }
+    if (c->n != n) c->n_changed = true;
+    c->n = n;
+    c->n_pad = n_pad;
+    c->depth = w->depth;
+    c->spp = w->spp;
+    c->have_world = true;
+    return RTX_OK;
+}
+
+int rtx_set_frame(rtx_ctx *c, const rtx_frame *f) {
+    if (!c || !f) return fail(RTX_ERR_INVALID, "rtx_set_frame: null argument");
+    if (f->width == 0 || f->height == 0)
+        return fail(RTX_ERR_INVALID, "rtx_set_frame: zero width or height");
+    if (f->rng_mode > 1) return fail(RTX_ERR_INVALID, "rtx_set_frame: unknown rng_mode");
+    if ((uint64_t)f->width * f->height > (1ull << 31))
+        return fail(RTX_ERR_INVALID, "rtx_set_frame: more than 2^31 pixels");
+    c->frame = *f;
+    c->have_frame = true;
+    return RTX_OK;
+}
+
+uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part, uint32_t nparts) {
+    if (tile_rows == 0 || nparts == 0 || part >= nparts) return 0;
+    const uint32_t tiles = (height + tile_rows - 1) / tile_rows;
+    if (part >= tiles) return 0;
+    const uint32_t my_tiles = (tiles - part + nparts - 1) / nparts;  // tiles part, part+nparts, ...
+    uint32_t rows = my_tiles * tile_rows;
+    const uint32_t last_tile = part + (my_tiles - 1) * nparts;
+    if (last_tile == tiles - 1) rows -= tiles * tile_rows - height;  // ragged final tile
+    return rows;
+}
+
+int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
+    if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_render_rows: no world uploaded");
+    if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_render_rows: no frame set");
+    if (tile_rows == 0 || nparts == 0 || part >= nparts)
+        return fail(RTX_ERR_INVALID, "rtx_render_rows: bad partition");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const rtx_frame &f = c->frame;
+    const uint32_t rows = rtx_part_rows(f.height, tile_rows, part, nparts);
+    float4 *out = reinterpret_cast<float4 *>(d_out);
+    if (!out) {
+        if (nparts != 1) return fail(RTX_ERR_INVALID, "rtx_render_rows: d_out NULL needs nparts == 1");
+        const size_t px = (size_t)f.width * f.height;
+        if (c->fb_pixels != px) {
+            RTX_HIP(hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_fb);
+            c->d_fb = nullptr;
+            c->fb_pixels = 0;
+            RTX_HIP(hipMalloc(&c->d_fb, px * sizeof(float4)));
+            c->fb_pixels = px;
+        }
+        out = c->d_fb;
+    }
+    rtx::KParams p{};
+    p.scene = scene_of(c);
+    p.out = out;
+    p.counters = c->d_counters;
+    p.depth = c->depth;
+    p.spp = c->spp;
+    p.width = f.width;
+    p.rows_local = rows;
+    p.tile_rows = tile_rows;
+    p.part = part;
+    p.nparts = nparts;
+    p.rng_mode = f.rng_mode;
+    p.frame_index = f.frame_index;
+    for (int k = 0; k < 3; ++k) {
+        p.org[k] = f.origin[k];
+        p.hor[k] = f.horizontal[k];
+        p.ver[k] = f.vertical[k];
+        p.llc[k] = f.lower_left[k];
+    }
+    p.img_w = f.img_w;
+    p.img_h = f.img_h;
+
+    if (c->events_used == c->events.size()) {
+        EventPair ev;
+        RTX_HIP(hipEventCreate(&ev.start));
+        RTX_HIP(hipEventCreate(&ev.stop));
+        c->events.push_back(ev);
+    }
+    EventPair &ev = c->events[c->events_used++];
+    RTX_HIP(hipEventRecord(ev.start, c->stream));
+    hipError_t e = rtx::launch_render(p, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_render");
+    RTX_HIP(hipEventRecord(ev.stop, c->stream));
+    c->launches++;
+    c->samples += (uint64_t)rows * f.width * c->spp;
+    return RTX_OK;
+}
+
+int rtx_render(rtx_ctx *c) { return rtx_render_rows(c, 1, 0, 1, nullptr); }
+
+int rtx_deinterleave_rows(rtx_ctx *c, const void *d_gathered, uint32_t width, uint32_t height,
+                          uint32_t tile_rows, uint32_t nparts, void *d_image) {
+    if (!c || !d_gathered || !d_image) return fail(RTX_ERR_INVALID, "rtx_deinterleave_rows: null argument");
+    if (tile_rows == 0 || nparts == 0) return fail(RTX_ERR_INVALID, "rtx_deinterleave_rows: bad partition");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const uint32_t max_rows = rtx_part_rows(height, tile_rows, 0, nparts);  // part 0 is largest
+    hipError_t e = rtx::launch_deinterleave(reinterpret_cast<const float4 *>(d_gathered),
+                                            reinterpret_cast<float4 *>(d_image), width, height,
+                                            tile_rows, nparts, max_rows, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_deinterleave");
+    return RTX_OK;
+}
+
+int rtx_sync(rtx_ctx *c) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_sync: null ctx");
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+void *rtx_framebuffer(rtx_ctx *c) { return c ? c->d_fb : nullptr; }
+
+int rtx_download(rtx_ctx *c, float *host, size_t bytes) {
+    if (!c || !host) return fail(RTX_ERR_INVALID, "rtx_download: null argument");
+    if (!c->d_fb) return fail(RTX_ERR_STATE, "rtx_download: nothing rendered into the context framebuffer");
+    if (bytes != c->fb_pixels * sizeof(float4))
+        return fail(RTX_ERR_INVALID, "rtx_download: bytes != width*height*16");
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    RTX_HIP(hipMemcpy(host, c->d_fb, bytes, hipMemcpyDeviceToHost));
+    return RTX_OK;
+}
+
+int rtx_stats_reset(rtx_ctx *c) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_stats_reset: null ctx");
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    RTX_HIP(hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)));
+    c->events_used = 0;
+    c->samples = 0;
+    c->launches = 0;
+    c->n_changed = false;
+    return RTX_OK;
+}
+
+int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
+    if (!c || !out) return fail(RTX_ERR_INVALID, "rtx_get_stats: null argument");
+    if (c->n_changed) return fail(RTX_ERR_STATE, "rtx_get_stats: world changed since rtx_stats_reset");
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long h[4];
+    RTX_HIP(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+    double ms = 0.0;
+    for (size_t i = 0; i < c->events_used; ++i) {
+        float t = 0.0f;
+        RTX_HIP(hipEventElapsedTime(&t, c->events[i].start, c->events[i].stop));
+        ms += t;
+    }
+    out->kernel_ms = ms;
+    out->launches = c->launches;
+    out->samples = c->samples;
+    out->segments = h[0];
+    out->sphere_tests = h[0] * (uint64_t)c->n;
+    return RTX_OK;
+}
+
+int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_min, float t_max,
+                        float *out) {
+    if (!c || (nrays && (!rays || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_hit_world: null argument");
+    if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_debug_hit_world: no world uploaded");
+    if (nrays == 0) return RTX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    float *d_rays = nullptr, *d_out = nullptr;
+    RTX_HIP(hipMalloc(&d_rays, (size_t)nrays * 6 * sizeof(float)));
+    hipError_t e = hipMalloc(&d_out, (size_t)nrays * 10 * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, (size_t)nrays * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtx::launch_debug_hit_world(scene_of(c), d_rays, nrays, t_min, t_max, d_out, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, (size_t)nrays * 10 * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return hip_fail(e, "rtx_debug_hit_world");
+    return RTX_OK;
+}
+
+int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint32_t n, float *out) {
+    if (!c || (n && (!in0 || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_math: null argument");
+    if (fn < RTX_FN_SQRT || fn > RTX_FN_RIUS) return fail(RTX_ERR_INVALID, "rtx_debug_math: unknown fn");
+    if (n == 0) return RTX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    float *d0 = nullptr, *d1 = nullptr, *dout = nullptr;
+    const size_t outn = (size_t)n * 3;
+    RTX_HIP(hipMalloc(&d0, (size_t)n * sizeof(float)));
+    hipError_t e = hipMalloc(&dout, outn * sizeof(float));
+    if (e == hipSuccess && in1) e = hipMalloc(&d1, (size_t)n * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(d0, in0, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess && in1) e = hipMemcpy(d1, in1, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(dout, 0, outn * sizeof(float));
+    if (e == hipSuccess) e = rtx::launch_debug_math(fn, d0, d1, n, dout, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const size_t copy_n = (fn >= RTX_FN_HASH1) ? outn : (size_t)n;
+    if (e == hipSuccess) e = hipMemcpy(out, dout, copy_n * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d0);
+    (void)hipFree(d1);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return hip_fail(e, "rtx_debug_math");
+    return RTX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// rtx_internal.h — kernel parameter block and launch entry points shared by
+// rtx_kernels.hip (device code) and rtx_api.hip (C-ABI context glue).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtx {
+
+// Device scene layout (structure of arrays, all in HBM, read-only):
+//   sph   float4[n]  center.xyz, -(radius*radius)  — streamed by every ray segment
+//   rad   float [n]  radius                  — read once per hit (normal)
+//   mtype int   [n]  material code 0/1/2, 3 = "no scatter"
+//   mval  float4[n]  albedo.rgb, fuzz-or-ir
+// `sph` is padded to n_pad = roundup(n, kPad) entries with copies of sphere
+// n-1; a padded copy can only win where sphere n-1 itself would (same data,
+// later index wins ties), so kernels clamp the winning index to n-1.
+struct KScene {
+    const float4 *sph;
+    const float *rad;
+    const int *mtype;
+    const float4 *mval;
+    uint32_t n, n_pad;
+};
+
+constexpr uint32_t kPad = 8;
+
+// Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
+struct KParams {
+    KScene scene;
+    float4 *out;                   // part's rows, contiguous, row-major
+    unsigned long long *counters;  // [0] += ray segments (hit_world calls)
+    uint32_t depth, spp;
+    uint32_t width, rows_local;    // launch covers rows_local * width lanes
+    uint32_t tile_rows, part, nparts;
+    uint32_t rng_mode, frame_index;
+    float org[3], hor[3], ver[3], llc[3];
+    float img_w, img_h;
+};
+
+// Spheres kept resident in LDS up to this count (16 B each); larger scenes
+// are streamed through LDS in chunks of kChunk spheres.
+constexpr uint32_t kResidentMax = 4096;  // 64 KiB
+constexpr uint32_t kChunk = 1024;        // 16 KiB
+constexpr uint32_t kBlock = 256;         // 4 waves
+
+hipError_t launch_render(const KParams &p, hipStream_t stream);
+hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,
+                               uint32_t height, uint32_t tile_rows, uint32_t nparts,
+                               uint32_t max_rows, hipStream_t stream);
+hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays,
+                                  float t_min, float t_max, float *out, hipStream_t stream);
+hipError_t launch_debug_math(int fn, const float *in0, const float *in1, uint32_t n,
+                             float *out, hipStream_t stream);
+
+}  // namespace rtx

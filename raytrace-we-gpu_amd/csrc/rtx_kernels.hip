@@ -1,0 +1,451 @@
+// rtx_kernels.hip — the hot path: CSMain / sample_color / hit_world /
+// hit_sphere / scatter of CSVersion/ShaderCompute.hlsl:155-315 as a CDNA4
+// (gfx950, wave64) HIP kernel.
+//
+// Design:
+//  * one lane per pixel, exact W x rows grid (the reference over-launches
+//    1024x1024 threads for 1024x576, DxCSApp.cpp:524 — no output difference);
+//  * the reference's RNG chain (one fp32 seed per pixel carried through all
+//    samples, ShaderCompute.hlsl:295,304-309) is kept, and the spp x depth
+//    double loop is flattened into a per-lane state machine: a lane whose
+//    path ends starts its pixel's next sample in the same iteration
+//    ("path regeneration"), so a wave's lanes all trace a segment on every
+//    iteration instead of idling while the longest path of the wave
+//    finishes;
+//  * hit_world is a linear closest-hit scan over the sphere array in index
+//    order (Hittable_list.cpp:3-20 / ShaderCompute.hlsl:188-205), spheres
+//    read from LDS by wave-uniform (broadcast) ds_read_b128: resident for
+//    n <= kResidentMax, streamed in kChunk tiles otherwise;
+//  * the quadratic's root/sqrt work sits behind the per-sphere "disc >= 0"
+//    branch, so a wave skips it when no lane's ray line meets the sphere
+//    (the wave-level early-out on all-miss);
+//  * the hit record (p, normal, front_face, material) is built once per
+//    segment for the winning sphere, not for every accepted candidate —
+//    identical values, because the reference's final record is the last
+//    accepted one.
+#include "rtx_device_math.h"
+#include "rtx_internal.h"
+
+namespace rtx {
+
+namespace {
+
+constexpr float kTMin = 0.001f;  // hit_world(cur_ray, 0.001, 1.#INF, h), :262
+
+struct Frame {
+    f3 org, hor, ver, llc;
+    float img_w, img_h;
+};
+
+// get_ray (ShaderCompute.hlsl:118-127): dir = llc + s*H + t*V - origin.
+__device__ __forceinline__ void get_ray(const Frame &F, float s, float t, f3 &o, f3 &d) {
+    o = F.org;
+    d = ((F.llc + s * F.hor) + t * F.ver) - F.org;
+}
+
+// CSMain's per-sample jitter (ShaderCompute.hlsl:306-307): two hash2 calls,
+// u takes .x of the first, v takes .y of the second.
+__device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_t y, float &seed,
+                                             f3 &o, f3 &d) {
+    float h0, h1, g0, g1;
+    hash2(seed, h0, h1);
+    const float u = ((float)x + h0 * 1.1f) / (F.img_w - 1.0f);
+    hash2(seed, g0, g1);
+    const float v = ((float)y + g1 * 1.1f) / (F.img_h - 1.0f);
+    get_ray(F, u, v, o, d);
+}
+
+// a = |d|^2 (Sphere.cpp:8; HLSL length(d)*length(d), :160), fma form.
+__device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y, d.y, d.x * d.x)); }
+
+// One ray against spheres [0, n) of `sph` (global indices base + i), in
+// index order. `best` is closest_so_far (t_max shrinks on every accepted
+// hit, :196-200); strict rejection `root < t_min || t_max < root` (:171,174)
+// lets a later sphere win an exact tie. Returns the winning index or `idx`.
+//
+// Per sphere ("hit_sphere"): oc = o - c; hb = oc.d;
+// cc = |oc|^2 - r^2; disc = hb^2 - a*cc; NaN disc falls through like the
+// reference's `if (d < 0) return false`.
+__device__ __forceinline__ float sphere_disc(const float4 s, f3 o, f3 d, float a, float &hb) {
+    const float ocx = o.x - s.x;
+    const float ocy = o.y - s.y;
+    const float ocz = o.z - s.z;
+    hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+    const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, s.w)));  // s.w = -r^2
+    return fmaf(hb, hb, -(a * cc));
+}
+// Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
+// the near one is outside [t_min, best] (Sphere.cpp:15-24).
+__device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, float t_min,
+                                             float &best, int &idx, int i) {
+    const float sq = sqrtf(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min || best < root);
+    if (!ok) {
+        root = (-hb + sq) * inv_a;
+        ok = !(root < t_min || best < root);
+    }
+    if (ok) {
+        best = root;
+        idx = i;
+    }
+}
+// n must be a multiple of kPad (the device array is padded with copies of
+// the last sphere; callers clamp the index to count-1, see pad_scene).
+// Four spheres per step: their LDS reads issue together, and one branch
+// skips all four when every lane's disc < 0 (wave-level all-miss early out).
+__device__ __forceinline__ int hit_range(const float4 *__restrict__ sph, uint32_t n,
+                                         uint32_t base, f3 o, f3 d, float a, float inv_a,
+                                         float t_min, float &best, int idx) {
+    for (uint32_t i = 0; i < n; i += 4) {
+        const float4 s0 = sph[i + 0];
+        const float4 s1 = sph[i + 1];
+        const float4 s2 = sph[i + 2];
+        const float4 s3 = sph[i + 3];
+        float hb0, hb1, hb2, hb3;
+        const float d0 = sphere_disc(s0, o, d, a, hb0);
+        const float d1 = sphere_disc(s1, o, d, a, hb1);
+        const float d2 = sphere_disc(s2, o, d, a, hb2);
+        const float d3 = sphere_disc(s3, o, d, a, hb3);
+        // Wave-uniform: skip the four root computations when no lane's ray
+        // line meets any of the four spheres.
+        const uint64_t any = __ballot(!(d0 < 0.0f)) | __ballot(!(d1 < 0.0f)) |
+                             __ballot(!(d2 < 0.0f)) | __ballot(!(d3 < 0.0f));
+        if (any != 0ull) {
+            const int g = (int)(base + i);
+            if (!(d0 < 0.0f)) sphere_roots(hb0, d0, inv_a, t_min, best, idx, g + 0);
+            if (!(d1 < 0.0f)) sphere_roots(hb1, d1, inv_a, t_min, best, idx, g + 1);
+            if (!(d2 < 0.0f)) sphere_roots(hb2, d2, inv_a, t_min, best, idx, g + 2);
+            if (!(d3 < 0.0f)) sphere_roots(hb3, d3, inv_a, t_min, best, idx, g + 3);
+        }
+    }
+    return idx;
+}
+
+// Lane state of one pixel's path tracer.
+struct Lane {
+    f3 o, d, col, acc;
+    float a, inv_a, seed;
+    uint32_t sample, bounce, segs;
+    bool active;
+};
+
+__device__ __forceinline__ void set_dir(Lane &L, f3 d) {
+    L.d = d;
+    L.a = dir_len2(d);
+    L.inv_a = 1.0f / L.a;
+}
+
+__device__ __forceinline__ float pixel_seed(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
+    // Reference: p = float(baseHash(DTid.xy)) / float(0xffffffffU)  (:295)
+    uint32_t h = base_hash(x, y);
+    if (P.rng_mode == 1u)  // per-sample re-seed (extension)
+        h = base_hash(h, P.frame_index * P.spp + s);
+    else if (P.frame_index != 0u)  // progressive frames (extension)
+        h = base_hash(h, 0x80000000u | P.frame_index);
+    return (float)h / 4294967296.0f;
+}
+
+__device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, uint32_t x, uint32_t y,
+                                             Lane &L) {
+    if (P.rng_mode == 1u) L.seed = pixel_seed(P, x, y, L.sample);
+    f3 o, d;
+    start_sample(F, x, y, L.seed, o, d);
+    L.o = o;
+    set_dir(L, d);
+    L.col = mk3(1.0f, 1.0f, 1.0f);
+    L.bounce = 0;
+}
+
+// Shading of one finished hit_world call (sample_color body, :262-284, and
+// scatter, :207-252). Advances the lane to its next sample when the path
+// ends; clears `active` after the pixel's last sample.
+__device__ __forceinline__ void shade(const KParams &P, const Frame &F, uint32_t x, uint32_t y,
+                                      Lane &L, int hit, float t) {
+    L.segs++;
+    bool ended = false;
+    if (hit >= 0) {
+        const KScene &S = P.scene;
+        const float4 sc = S.sph[hit];
+        const f3 p = L.o + t * L.d;                    // Ray::at, Ray.h:16-19
+        const float inv_r = 1.0f / S.rad[hit];         // Vec3 operator/, Vec3.h:83-86
+        f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));  // Sphere.cpp:28
+        const bool ff = dot3(L.d, nrm) < 0.0f;         // set_face_normal, :143-150
+        if (!ff) nrm = -nrm;
+        const int mt = S.mtype[hit];
+        const float4 mv = S.mval[hit];
+        f3 dir;
+        bool scattered = true;
+        if (mt == 0) {  // DIFFUSE (:209-217)
+            const f3 rius = random_in_unit_sphere(L.seed);
+            const f3 target = (p + nrm) + rius;
+            dir = normalize3(target - p);
+            L.col = L.col * mk3(mv.x, mv.y, mv.z);
+        } else if (mt == 1) {  // METAL (:219-227), always scatters
+            const f3 refl = reflect3(L.d, nrm);
+            const f3 rius = random_in_unit_sphere(L.seed);
+            dir = normalize3(refl + mv.w * rius);
+            L.col = L.col * mk3(mv.x, mv.y, mv.z);
+        } else if (mt == 2) {  // DIELECTRIC (:229-249), atten = 1
+            const float ratio = ff ? (1.0f / mv.w) : mv.w;
+            const f3 ud = normalize3(L.d);
+            const float cosine = fminf(dot3(-ud, nrm), 1.0f);
+            const float sine = sqrtf(1.0f - cosine * cosine);
+            const bool cant = ratio * sine > 1.0f;
+            // FXC's `||` does not short-circuit: hash1 always advances the seed.
+            const float refl = reflectance(cosine, ratio);
+            const float h = hash1(L.seed);
+            dir = (cant || refl > h) ? reflect3(ud, nrm) : refract3(ud, nrm, ratio);
+        } else {
+            scattered = false;  // unknown material: sample is black (:251, :274)
+        }
+        if (scattered) {
+            L.o = p;
+            set_dir(L, dir);
+            L.bounce++;
+            ended = L.bounce >= P.depth;  // depth exhausted -> black (:286)
+        } else {
+            ended = true;
+        }
+    } else {  // miss: sky gradient (:279-283)
+        const f3 ud = normalize3(L.d);
+        const float tt = 0.5f * (ud.y + 1.0f);
+        const float w = 1.0f - tt;
+        const f3 sky = mk3(w + tt * 0.5f, w + tt * 0.7f, w + tt);
+        L.acc = L.acc + L.col * sky;
+        ended = true;
+    }
+    if (ended) {
+        L.sample++;
+        if (L.sample >= P.spp)
+            L.active = false;
+        else
+            begin_sample(P, F, x, y, L);
+    }
+}
+
+__device__ __forceinline__ void lane_pixel(const KParams &P, uint32_t gid, uint32_t &x, uint32_t &y) {
+    const uint32_t lr = gid / P.width;  // local row
+    x = gid - lr * P.width;
+    const uint32_t j = lr / P.tile_rows;
+    const uint32_t w = lr - j * P.tile_rows;
+    y = (j * P.nparts + P.part) * P.tile_rows + w;
+}
+
+__device__ __forceinline__ void finish(const KParams &P, uint32_t gid, const Lane &L, bool valid) {
+    // Segment counter: wave sum, one 64-bit atomic per wave.
+    uint32_t segs = valid ? L.segs : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
+    if ((threadIdx.x & 63u) == 0u && segs != 0u)
+        atomicAdd(P.counters, (unsigned long long)segs);
+    if (valid) {
+        // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
+        const float spp = (float)P.spp;
+        float4 o;
+        o.x = to_gamma(L.acc.x / spp);
+        o.y = to_gamma(L.acc.y / spp);
+        o.z = to_gamma(L.acc.z / spp);
+        o.w = 1.0f;
+        P.out[gid] = o;
+    }
+}
+
+__device__ __forceinline__ Frame load_frame(const KParams &P) {
+    Frame F;
+    F.org = mk3(P.org[0], P.org[1], P.org[2]);
+    F.hor = mk3(P.hor[0], P.hor[1], P.hor[2]);
+    F.ver = mk3(P.ver[0], P.ver[1], P.ver[2]);
+    F.llc = mk3(P.llc[0], P.llc[1], P.llc[2]);
+    F.img_w = P.img_w;
+    F.img_h = P.img_h;
+    return F;
+}
+
+__device__ __forceinline__ void init_lane(const KParams &P, const Frame &F, uint32_t x, uint32_t y,
+                                          bool valid, Lane &L) {
+    L.acc = mk3(0.0f, 0.0f, 0.0f);
+    L.col = mk3(1.0f, 1.0f, 1.0f);
+    L.o = mk3(0.0f, 0.0f, 0.0f);
+    L.d = mk3(0.0f, 0.0f, 1.0f);
+    L.a = 1.0f;
+    L.inv_a = 1.0f;
+    L.sample = 0;
+    L.bounce = 0;
+    L.segs = 0;
+    L.seed = valid ? pixel_seed(P, x, y, 0) : 0.0f;
+    // depth 0: every sample returns black without tracing (:260, :286).
+    L.active = valid && P.spp > 0u && P.depth > 0u;
+    if (L.active) begin_sample(P, F, x, y, L);
+}
+
+// Scene resident in LDS (n <= kResidentMax): waves run independently.
+__global__ void __launch_bounds__(kBlock) k_render_resident(const KParams P) {
+    extern __shared__ float4 s_sph[];
+    const uint32_t n = P.scene.n_pad;
+    const int last = (int)P.scene.n - 1;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) s_sph[i] = P.scene.sph[i];
+    __syncthreads();
+
+    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = gid < P.rows_local * P.width;
+    uint32_t x = 0, y = 0;
+    if (valid) lane_pixel(P, gid, x, y);
+    const Frame F = load_frame(P);
+    Lane L;
+    init_lane(P, F, x, y, valid, L);
+
+    while (__ballot(L.active) != 0ull) {
+        if (L.active) {
+            float best = __uint_as_float(0x7f800000u);
+            const int hit = hit_range(s_sph, n, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+            shade(P, F, x, y, L, min(hit, last), best);
+        }
+    }
+    finish(P, gid, L, valid);
+}
+
+// Large scenes: every ray segment streams the sphere array through LDS in
+// kChunk-sphere tiles shared by the block's 4 waves (block-synchronous).
+__global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
+    extern __shared__ float4 s_sph[];
+    const uint32_t n = P.scene.n_pad;
+    const int last = (int)P.scene.n - 1;
+    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = gid < P.rows_local * P.width;
+    uint32_t x = 0, y = 0;
+    if (valid) lane_pixel(P, gid, x, y);
+    const Frame F = load_frame(P);
+    Lane L;
+    init_lane(P, F, x, y, valid, L);
+
+    while (__syncthreads_or(L.active ? 1 : 0)) {
+        float best = __uint_as_float(0x7f800000u);
+        int hit = -1;
+        for (uint32_t base = 0; base < n; base += kChunk) {
+            const uint32_t cnt = min(kChunk, n - base);
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < cnt; i += kBlock) s_sph[i] = P.scene.sph[base + i];
+            __syncthreads();
+            if (L.active) hit = hit_range(s_sph, cnt, base, L.o, L.d, L.a, L.inv_a, kTMin, best, hit);
+        }
+        if (L.active) shade(P, F, x, y, L, min(hit, last), best);
+    }
+    finish(P, gid, L, valid);
+}
+
+// Gathered [nparts][max_rows][width] -> image [height][width].
+__global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restrict__ g,
+                                                         float4 *__restrict__ img, uint32_t width,
+                                                         uint32_t height, uint32_t tile_rows,
+                                                         uint32_t nparts, uint32_t max_rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (uint64_t)width * height) return;
+    const uint32_t y = (uint32_t)(i / width);
+    const uint32_t x = (uint32_t)(i - (uint64_t)y * width);
+    const uint32_t tile = y / tile_rows;
+    const uint32_t part = tile % nparts;
+    const uint32_t lr = (tile / nparts) * tile_rows + (y - tile * tile_rows);
+    img[i] = g[((uint64_t)part * max_rows + lr) * width + x];
+}
+
+__global__ void __launch_bounds__(kBlock) k_debug_hit_world(const KScene S, const float *rays,
+                                                            uint32_t nrays, float t_min,
+                                                            float t_max, float *out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nrays) return;
+    const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
+    const f3 d = mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    const float a = dir_len2(d);
+    const float inv_a = 1.0f / a;
+    float best = t_max;
+    const int idx = min(hit_range(S.sph, S.n_pad, 0, o, d, a, inv_a, t_min, best, -1), (int)S.n - 1);
+    float *r = out + 10 * (size_t)i;
+    if (idx < 0) {
+        for (int k = 0; k < 10; ++k) r[k] = 0.0f;
+        r[9] = -1.0f;
+        return;
+    }
+    const float4 sc = S.sph[idx];
+    const f3 p = o + best * d;
+    const float inv_r = 1.0f / S.rad[idx];
+    f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));
+    const bool ff = dot3(d, nrm) < 0.0f;
+    if (!ff) nrm = -nrm;
+    r[0] = 1.0f;
+    r[1] = best;
+    r[2] = p.x; r[3] = p.y; r[4] = p.z;
+    r[5] = nrm.x; r[6] = nrm.y; r[7] = nrm.z;
+    r[8] = ff ? 1.0f : 0.0f;
+    r[9] = (float)idx;
+}
+
+__global__ void __launch_bounds__(kBlock) k_debug_math(int fn, const float *in0, const float *in1,
+                                                       uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float a = in0[i];
+    const float b = in1 ? in1[i] : 0.0f;
+    float seed = a;
+    switch (fn) {
+        case 0: out[i] = sqrtf(a); break;
+        case 1: out[i] = a / b; break;
+        case 2: { float s, c; sincos_rt(a, s, c); out[i] = s; } break;
+        case 3: { float s, c; sincos_rt(a, s, c); out[i] = c; } break;
+        case 4: out[i] = log2_rt(a); break;
+        case 5: out[i] = exp2_rt(a); break;
+        case 6: out[i] = pow_rt(a, b); break;
+        case 7: out[i] = __uint_as_float(base_hash(__float_as_uint(a), __float_as_uint(b))); break;
+        case 8: out[3 * i] = hash1(seed); out[3 * i + 1] = seed; out[3 * i + 2] = 0.0f; break;
+        case 9: hash2(seed, out[3 * i], out[3 * i + 1]); out[3 * i + 2] = seed; break;
+        case 10: { const f3 h = hash3(seed); out[3 * i] = h.x; out[3 * i + 1] = h.y; out[3 * i + 2] = h.z; } break;
+        case 11: { const f3 r = random_in_unit_sphere(seed); out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z; } break;
+        default: out[i] = 0.0f;
+    }
+}
+
+inline uint32_t ceil_div(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_render(const KParams &p, hipStream_t stream) {
+    const uint64_t lanes = (uint64_t)p.rows_local * p.width;
+    if (lanes == 0) return hipSuccess;
+    const uint32_t blocks = ceil_div(lanes, kBlock);
+    if (p.scene.n_pad <= kResidentMax) {
+        const size_t lds = (size_t)(p.scene.n_pad ? p.scene.n_pad : 1) * sizeof(float4);
+        hipLaunchKernelGGL(k_render_resident, dim3(blocks), dim3(kBlock), lds, stream, p);
+    } else {
+        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kBlock), kChunk * sizeof(float4),
+                           stream, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,
+                               uint32_t height, uint32_t tile_rows, uint32_t nparts,
+                               uint32_t max_rows, hipStream_t stream) {
+    const uint64_t n = (uint64_t)width * height;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_deinterleave, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, gathered,
+                       image, width, height, tile_rows, nparts, max_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays, float t_min,
+                                  float t_max, float *out, hipStream_t stream) {
+    if (nrays == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kBlock)), dim3(kBlock), 0, stream, s,
+                       rays, nrays, t_min, t_max, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_math(int fn, const float *in0, const float *in1, uint32_t n, float *out,
+                             hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_debug_math, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, fn, in0, in1,
+                       n, out);
+    return hipGetLastError();
+}
+
+}  // namespace rtx

@@ -1,0 +1,307 @@
+"""rtx — Python host binding of librtx.so (the MI355X path tracer's C-ABI).
+
+Thin ctypes layer over ``include/rtx.h``; the compute path is the HIP kernel
+in ``raytrace-we-gpu_amd/csrc``. There is deliberately no CPU fallback: if
+``librtx.so`` is missing, importing the GPU entry points raises.
+
+Host surface mirrors the reference app (CSVersion/DxCSApp.cpp):
+  * :func:`random_world` / :func:`test_world`  ~ WorldDef::random_world /
+    test_world (DxCSApp.cpp:72-157)
+  * :func:`camera_look_at`                    ~ PerFrame::ComputeViewVals
+    (DxCSApp.cpp:39-61) + focus distance (:488)
+  * :class:`Context`                           ~ CDx11Base + DxCSApp resource
+    lifetime (upload_world = WorldDef cbuffer, set_frame = PerFrame cbuffer,
+    render_rows = Dispatch, DxCSApp.cpp:524)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RTX_LIB", os.path.join(_PKG_DIR, "lib", "librtx.so"))
+
+RTX_OK = 0
+MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
+RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
+FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
+          hash1=8, hash2=9, hash3=10, rius=11)
+
+
+class RtxError(RuntimeError):
+    pass
+
+
+class rtx_world(C.Structure):
+    _fields_ = [("count", C.c_uint32), ("depth", C.c_uint32), ("spp", C.c_uint32),
+                ("reserved", C.c_uint32), ("spheres", C.POINTER(C.c_float)),
+                ("mat_types", C.POINTER(C.c_float)), ("mat_values", C.POINTER(C.c_float))]
+
+
+class rtx_frame(C.Structure):
+    _fields_ = [("origin", C.c_float * 4), ("horizontal", C.c_float * 4),
+                ("vertical", C.c_float * 4), ("lower_left", C.c_float * 4),
+                ("img_w", C.c_float), ("img_h", C.c_float), ("width", C.c_uint32),
+                ("height", C.c_uint32), ("rng_mode", C.c_uint32), ("frame_index", C.c_uint32),
+                ("reserved", C.c_uint32 * 2)]
+
+
+class rtx_stats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_uint64), ("samples", C.c_uint64),
+                ("segments", C.c_uint64), ("sphere_tests", C.c_uint64)]
+
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None) -> C.CDLL:
+    """Load librtx.so (raises RtxError if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RtxError(f"librtx.so not found at {p}: build it first (python -c "
+                       "'import __graft_entry__ as g; g.build()' or make)")
+    lib = C.CDLL(p)
+    f, u32, i32, vp = C.POINTER(C.c_float), C.c_uint32, C.c_int32, C.c_void_p
+    ctx = C.c_void_p
+    sig = {
+        "rtx_version": (C.c_int, []),
+        "rtx_last_error": (C.c_char_p, []),
+        "rtx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "rtx_create": (C.c_int, [C.c_int, C.POINTER(ctx)]),
+        "rtx_destroy": (None, [ctx]),
+        "rtx_set_stream": (C.c_int, [ctx, vp]),
+        "rtx_upload_world": (C.c_int, [ctx, C.POINTER(rtx_world)]),
+        "rtx_set_frame": (C.c_int, [ctx, C.POINTER(rtx_frame)]),
+        "rtx_render_rows": (C.c_int, [ctx, u32, u32, u32, vp]),
+        "rtx_render": (C.c_int, [ctx]),
+        "rtx_part_rows": (u32, [u32, u32, u32, u32]),
+        "rtx_deinterleave_rows": (C.c_int, [ctx, vp, u32, u32, u32, u32, vp]),
+        "rtx_sync": (C.c_int, [ctx]),
+        "rtx_framebuffer": (vp, [ctx]),
+        "rtx_download": (C.c_int, [ctx, f, C.c_size_t]),
+        "rtx_stats_reset": (C.c_int, [ctx]),
+        "rtx_get_stats": (C.c_int, [ctx, C.POINTER(rtx_stats)]),
+        "rtx_scene_random_world": (C.c_int, [i32, u32, f, f, f, C.POINTER(u32)]),
+        "rtx_scene_test_world": (C.c_int, [f, f, f, C.POINTER(u32)]),
+        "rtx_camera_look_at": (C.c_int, [f, f, f, C.c_float, C.c_float, C.c_float, C.c_float,
+                                         u32, u32, C.POINTER(rtx_frame)]),
+        "rtx_camera_simple": (C.c_int, [u32, u32, C.POINTER(rtx_frame)]),
+        "rtx_world_from_worlddef": (C.c_int, [vp, C.c_size_t, f, f, f, C.POINTER(rtx_world)]),
+        "rtx_frame_from_perframe": (C.c_int, [vp, C.c_size_t, u32, u32, C.POINTER(rtx_frame)]),
+        "rtx_debug_hit_world": (C.c_int, [ctx, f, u32, C.c_float, C.c_float, f]),
+        "rtx_debug_math": (C.c_int, [ctx, C.c_int, f, f, u32, f]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _check(rc: int, what: str):
+    if rc != RTX_OK:
+        msg = load_library().rtx_last_error().decode(errors="replace")
+        raise RtxError(f"{what} failed ({rc}): {msg}")
+
+
+# ---------------------------------------------------------------------------
+# Scene / camera producers (host-side, no GPU)
+# ---------------------------------------------------------------------------
+@dataclass
+class World:
+    """Scene ~ WorldDef (DxCSApp.cpp:64-71): spheres [n,4] (center, radius),
+    mat_types [n] (0 Lambert, 1 metal, 2 dielectric), mat_values [n,4]."""
+    spheres: np.ndarray
+    mat_types: np.ndarray
+    mat_values: np.ndarray
+    depth: int = 50
+    spp: int = 60
+
+    @property
+    def count(self) -> int:
+        return int(self.spheres.shape[0])
+
+    def as_struct(self):
+        self.spheres = np.ascontiguousarray(self.spheres, dtype=np.float32)
+        self.mat_types = np.ascontiguousarray(self.mat_types, dtype=np.float32)
+        self.mat_values = np.ascontiguousarray(self.mat_values, dtype=np.float32)
+        w = rtx_world()
+        w.count, w.depth, w.spp, w.reserved = self.count, self.depth, self.spp, 0
+        w.spheres, w.mat_types, w.mat_values = (_fptr(self.spheres), _fptr(self.mat_types),
+                                                _fptr(self.mat_values))
+        return w
+
+
+def random_world(grid_half_extent: int = 9, capacity: Optional[int] = None, depth: int = 50,
+                 spp: int = 60) -> World:
+    """WorldDef::random_world (DxCSApp.cpp:72-134). 9 -> 326 spheres (the
+    reference scene), 11 -> 486 (RTIOW final scene), 159 -> 101,124."""
+    cap = capacity if capacity is not None else 4 + (2 * grid_half_extent) ** 2
+    sph = np.zeros((cap, 4), np.float32)
+    mt = np.zeros(cap, np.float32)
+    mv = np.zeros((cap, 4), np.float32)
+    n = C.c_uint32()
+    _check(load_library().rtx_scene_random_world(grid_half_extent, cap, _fptr(sph), _fptr(mt),
+                                                 _fptr(mv), C.byref(n)), "rtx_scene_random_world")
+    k = n.value
+    return World(sph[:k].copy(), mt[:k].copy(), mv[:k].copy(), depth, spp)
+
+
+def test_world(depth: int = 50, spp: int = 50) -> World:
+    """WorldDef::test_world (DxCSApp.cpp:136-157)."""
+    sph = np.zeros((4, 4), np.float32)
+    mt = np.zeros(4, np.float32)
+    mv = np.zeros((4, 4), np.float32)
+    n = C.c_uint32()
+    _check(load_library().rtx_scene_test_world(_fptr(sph), _fptr(mt), _fptr(mv), C.byref(n)),
+           "rtx_scene_test_world")
+    return World(sph, mt, mv, depth, spp)
+
+
+def camera_look_at(width: int, height: int, look_from=(13.0, 2.0, 3.0), look_at=(0.0, 0.0, 0.0),
+                   vup=(0.0, 1.0, 0.0), vfov: float = 20.0, aspect: float = 16.0 / 9.0,
+                   aperture: float = 2.0, focus_dist: float = 0.0) -> rtx_frame:
+    """PerFrame::ComputeViewVals with DxCSApp's defaults (DxCSApp.cpp:176-179)."""
+    f = rtx_frame()
+    a = [np.asarray(v, np.float32) for v in (look_from, look_at, vup)]
+    _check(load_library().rtx_camera_look_at(_fptr(a[0]), _fptr(a[1]), _fptr(a[2]), vfov,
+                                             np.float32(aspect), aperture, focus_dist, width,
+                                             height, C.byref(f)), "rtx_camera_look_at")
+    return f
+
+
+def camera_simple(width: int, height: int) -> rtx_frame:
+    """Camera(width, height) of the CPU library (Camera.h:9-21)."""
+    f = rtx_frame()
+    _check(load_library().rtx_camera_simple(width, height, C.byref(f)), "rtx_camera_simple")
+    return f
+
+
+def part_rows(height: int, tile_rows: int, part: int, nparts: int) -> int:
+    return int(load_library().rtx_part_rows(height, tile_rows, part, nparts))
+
+
+def part_row_ids(height: int, tile_rows: int, part: int, nparts: int) -> np.ndarray:
+    """Global rows owned by `part` (interleaved tiles), ascending."""
+    y = np.arange(height, dtype=np.int64)
+    return y[(y // tile_rows) % nparts == part].astype(np.uint32)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = load_library().rtx_device_count(C.byref(n))
+    return n.value if rc == RTX_OK else 0
+
+
+# ---------------------------------------------------------------------------
+# GPU context
+# ---------------------------------------------------------------------------
+class Context:
+    """One HIP device's renderer (~ CDx11Base::Initialize .. Terminate)."""
+
+    def __init__(self, device: int = 0, stream: Optional[int] = None):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.rtx_create(device, C.byref(h)), "rtx_create")
+        self._h = h
+        self.device = device
+        self.frame: Optional[rtx_frame] = None
+        self.world: Optional[World] = None
+        if stream is not None:
+            self.set_stream(stream)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rtx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream: Optional[int]):
+        _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream or 0)), "rtx_set_stream")
+
+    def upload_world(self, world: World):
+        w = world.as_struct()
+        _check(self._lib.rtx_upload_world(self._h, C.byref(w)), "rtx_upload_world")
+        self.world = world
+
+    def set_frame(self, frame: rtx_frame):
+        _check(self._lib.rtx_set_frame(self._h, C.byref(frame)), "rtx_set_frame")
+        self.frame = frame
+
+    def render_rows(self, tile_rows: int, part: int, nparts: int, d_out: Optional[int] = None):
+        _check(self._lib.rtx_render_rows(self._h, tile_rows, part, nparts,
+                                         C.c_void_p(d_out or 0)), "rtx_render_rows")
+
+    def render(self):
+        _check(self._lib.rtx_render(self._h), "rtx_render")
+
+    def deinterleave(self, d_gathered: int, width: int, height: int, tile_rows: int, nparts: int,
+                     d_image: int):
+        _check(self._lib.rtx_deinterleave_rows(self._h, C.c_void_p(d_gathered), width, height,
+                                               tile_rows, nparts, C.c_void_p(d_image)),
+               "rtx_deinterleave_rows")
+
+    def sync(self):
+        _check(self._lib.rtx_sync(self._h), "rtx_sync")
+
+    def framebuffer_ptr(self) -> int:
+        return int(self._lib.rtx_framebuffer(self._h) or 0)
+
+    def download(self) -> np.ndarray:
+        f = self.frame
+        out = np.empty((f.height, f.width, 4), np.float32)
+        _check(self._lib.rtx_download(self._h, _fptr(out), out.nbytes), "rtx_download")
+        return out
+
+    def render_image(self) -> np.ndarray:
+        self.render()
+        return self.download()
+
+    def stats_reset(self):
+        _check(self._lib.rtx_stats_reset(self._h), "rtx_stats_reset")
+
+    def stats(self) -> rtx_stats:
+        s = rtx_stats()
+        _check(self._lib.rtx_get_stats(self._h, C.byref(s)), "rtx_get_stats")
+        return s
+
+    def debug_hit_world(self, rays: np.ndarray, t_min: float = 0.001,
+                        t_max: float = float("inf")) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        out = np.zeros((rays.shape[0], 10), np.float32)
+        _check(self._lib.rtx_debug_hit_world(self._h, _fptr(rays), rays.shape[0], t_min, t_max,
+                                             _fptr(out)), "rtx_debug_hit_world")
+        return out
+
+    def debug_math(self, fn: str, in0: np.ndarray, in1: Optional[np.ndarray] = None) -> np.ndarray:
+        a = np.ascontiguousarray(in0, np.float32)
+        b = None if in1 is None else np.ascontiguousarray(in1, np.float32)
+        out = np.zeros(3 * a.size, np.float32)
+        _check(self._lib.rtx_debug_math(self._h, FN[fn], _fptr(a),
+                                        _fptr(b) if b is not None else None, a.size, _fptr(out)),
+               "rtx_debug_math")
+        return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]

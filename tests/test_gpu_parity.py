@@ -1,0 +1,241 @@
+"""GPU parity tests: the HIP path (librtx.so, through the C-ABI) against the
+CPU oracle. The bar is bit-exact: the kernel and the oracle execute the
+same IEEE-754 fp32 operation sequence, so every pixel,
+every hit record and every math-function output must have identical bits
+(NaNs compare equal to NaNs). Against the reference's fp64 geometry the
+stated fp32 tolerance of tests/tolerance.py applies.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from tolerance import check_hits_against_fp64
+
+pytestmark = pytest.mark.gpu
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    assert a.shape == b.shape
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    return same
+
+
+def assert_bits_equal(a, b, what=""):
+    same = bits_equal(a, b)
+    if not same.all():
+        bad = np.argwhere(~same)
+        raise AssertionError(f"{what}: {(~same).sum()} of {same.size} values differ; first at "
+                             f"{bad[:5].tolist()}: gpu {np.asarray(a)[tuple(bad[0])]} vs oracle "
+                             f"{np.asarray(b)[tuple(bad[0])]}")
+
+
+# ---------------------------------------------------------------------------
+# function-level parity
+# ---------------------------------------------------------------------------
+def _math_inputs(fn):
+    rng = np.random.default_rng(sum(map(ord, fn)))
+    if fn == "sqrt":
+        return np.concatenate([rng.uniform(0, 10, 4000), 10.0 ** rng.uniform(-44, 38, 4000),
+                               [0.0, -0.0, np.inf, -1.0, np.nan, 1e-45]]).astype(np.float32), None
+    if fn == "div":
+        a = np.concatenate([rng.normal(size=4000), 10.0 ** rng.uniform(-30, 30, 4000)])
+        b = np.concatenate([rng.normal(size=4000), 10.0 ** rng.uniform(-30, 30, 4000)])
+        return a.astype(np.float32), b.astype(np.float32)
+    if fn in ("sin", "cos"):
+        return np.concatenate([rng.uniform(0, 2 * np.pi, 6000), rng.uniform(-20, 20, 2000),
+                               [0.0, np.float32(6.28318530718), np.pi / 2]]).astype(np.float32), None
+    if fn == "log2":
+        return np.concatenate([rng.uniform(0, 4, 3000), 10.0 ** rng.uniform(-44, 38, 5000),
+                               [1.0, 2.0, 0.5, 1e-45, 1.17549435e-38]]).astype(np.float32), None
+    if fn == "exp2":
+        return np.concatenate([rng.uniform(-2, 2, 3000), rng.uniform(-160, 135, 5000),
+                               [0.0, -126.0, -149.0, -150.0, 127.5, 128.0, np.nan]]).astype(np.float32), None
+    if fn == "pow":
+        a = np.concatenate([rng.uniform(0, 1, 3000), rng.uniform(0, 3, 3000), [0.0, 1.0, -1.0, np.inf, np.nan, 1e-40]])
+        b = np.concatenate([np.full(3000, 1 / 3), rng.choice([0.454545454545, 5.0, 2.0], 3000), np.full(6, 1 / 3)])
+        return a.astype(np.float32), b.astype(np.float32)
+    if fn == "basehash":
+        u = rng.integers(0, 2**32, size=(2, 8000), dtype=np.uint64).astype(np.uint32)
+        return u[0].view(np.float32), u[1].view(np.float32)
+    # hash1/2/3, rius: seeds
+    return np.concatenate([rng.uniform(0, 1, 6000), rng.uniform(0, 40, 2000)]).astype(np.float32), None
+
+
+@pytest.mark.parametrize("fn", ["sqrt", "div", "sin", "cos", "log2", "exp2", "pow", "basehash",
+                                "hash1", "hash2", "hash3", "rius"])
+def test_device_math_bit_exact(gpu_ctx, oracle, fn):
+    a, b = _math_inputs(fn)
+    got = gpu_ctx.debug_math(fn, a, b)
+    want = oracle.math(fn, a, b)
+    assert_bits_equal(got, want, fn)
+
+
+# ---------------------------------------------------------------------------
+# hit_world parity against the reference's golden vectors
+# ---------------------------------------------------------------------------
+def _golden_cases():
+    for name in ("hit_test_world.json", "hit_rtiow9.json"):
+        d = json.load(open(os.path.join(GOLDEN, name)))
+        for k in range(len(d["cases"])):
+            yield pytest.param(name, k, id=f"{name}-{k}")
+
+
+@pytest.mark.parametrize("name,k", list(_golden_cases()))
+def test_hit_world_golden(gpu_ctx, oracle, rtx, name, k):
+    d = json.load(open(os.path.join(GOLDEN, name)))
+    c = d["cases"][k]
+    t_max = np.inf if c["t_max"] is None else c["t_max"]
+    sph = np.array(d["spheres"], np.float32)
+    world = rtx.World(sph, np.zeros(len(sph), np.float32), np.zeros((len(sph), 4), np.float32), 1, 1)
+    gpu_ctx.upload_world(world)
+    rays = np.array(d["rays"])
+    got = gpu_ctx.debug_hit_world(rays.astype(np.float32), c["t_min"], t_max)
+    assert_bits_equal(got, oracle.hit_world_f32(world, rays.astype(np.float32), c["t_min"], t_max),
+                      "hit_world vs fp32 twin")
+    check_hits_against_fp64(d["spheres"], rays, got, c["expected"])
+
+
+def test_hit_world_ties_and_padding(gpu_ctx, oracle, rtx):
+    """Exact-t ties: the later sphere wins (strict `t_max < root`, ShaderCompute.hlsl:171).
+    Counts not a multiple of the device padding (8) exercise the padded copies."""
+    rng = np.random.default_rng(7)
+    for n in (1, 2, 7, 9, 13):
+        sph = np.concatenate([rng.uniform(-3, 3, (n, 3)), rng.uniform(0.2, 1.0, (n, 1))], 1).astype(np.float32)
+        sph[n // 2] = sph[0]  # duplicate -> ties
+        sph[-1] = sph[0] if n > 2 else sph[-1]
+        world = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
+        gpu_ctx.upload_world(world)
+        o = rng.uniform(-6, 6, (500, 3))
+        d = (sph[rng.integers(0, n, 500), :3] - o) + rng.normal(scale=0.2, size=(500, 3))
+        rays = np.concatenate([o, d], 1).astype(np.float32)
+        got = gpu_ctx.debug_hit_world(rays)
+        want = oracle.hit_world_f32(world, rays)
+        assert_bits_equal(got, want, f"n={n}")
+        if n > 2:
+            hit0 = want[:, 9] >= 0
+            assert not np.any(np.isin(want[hit0, 9], [0])), "tie must go to the later duplicate"
+
+
+# ---------------------------------------------------------------------------
+# whole-frame parity
+# ---------------------------------------------------------------------------
+def render_gpu(ctx, world, frame):
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    ctx.stats_reset()
+    img = ctx.render_image()
+    return img, ctx.stats()
+
+
+def test_c1_full_frame_bit_exact(gpu_ctx, oracle, rtx):
+    """C1: 400x225 test_world, Camera.h, spp 20, depth 12 — every pixel bit-exact,
+    and equal to the committed golden rows of the oracle."""
+    world = rtx.test_world(depth=12, spp=20)
+    frame = rtx.camera_simple(400, 225)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(225), nthreads=8)
+    assert_bits_equal(img, want, "C1 image")
+    assert st.segments == segs
+    gold = np.load(os.path.join(GOLDEN, "c1_oracle_rows.npz"))
+    assert_bits_equal(img[gold["rows"]], gold["pixels"], "C1 golden rows")
+
+
+@pytest.mark.parametrize("ext,w,h,spp,depth,rng_mode", [
+    (11, 192, 108, 6, 50, 0),
+    (9, 160, 90, 4, 50, 0),
+    (11, 96, 54, 5, 50, 1),
+    (3, 33, 17, 3, 7, 0),
+])
+def test_random_world_frames_bit_exact(gpu_ctx, oracle, rtx, ext, w, h, spp, depth, rng_mode):
+    world = rtx.random_world(ext, depth=depth, spp=spp)
+    frame = rtx.camera_look_at(w, h, aspect=w / h)
+    frame.rng_mode = rng_mode
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(h), nthreads=8)
+    assert_bits_equal(img, want, f"random_world({ext}) {w}x{h}")
+    assert st.segments == segs
+    assert st.sphere_tests == segs * world.count
+
+
+def test_c2_full_size_row_subset(gpu_ctx, oracle, rtx):
+    """C2 at full size: 1920x1080, RTIOW final scene (486 spheres), spp 100,
+    depth 50. The oracle renders every 24th row (45 rows, 8.6 M samples);
+    those rows must be bit-identical in the GPU frame."""
+    world = rtx.random_world(11, depth=50, spp=100)
+    frame = rtx.camera_look_at(1920, 1080)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    rows = np.arange(7, 1080, 24)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img[rows], want, "C2 rows")
+    assert np.isfinite(img).all()
+    assert st.samples == 1920 * 1080 * 100
+
+
+def test_c5_streamed_100k_spheres(gpu_ctx, oracle, rtx):
+    """C5 shape: 100,000 spheres (> LDS-resident limit -> streamed kernel)."""
+    world = rtx.random_world(159, capacity=100000, depth=50, spp=2)
+    frame = rtx.camera_look_at(48, 27, aspect=48 / 27)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(27), nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img, want, "100k spheres")
+    assert st.segments == segs
+
+
+def test_edge_cases(gpu_ctx, oracle, rtx):
+    """Empty scene (all sky), spp 0 (0/0 = NaN, as accColor /= 0), depth 0
+    (black), unknown material code (no scatter -> black), 1x1 frame."""
+    base = rtx.random_world(2, depth=10, spp=3)
+    empty = rtx.World(np.zeros((0, 4), np.float32), np.zeros(0, np.float32), np.zeros((0, 4), np.float32), 5, 3)
+    odd = rtx.World(base.spheres.copy(), base.mat_types.copy(), base.mat_values.copy(), 10, 3)
+    odd.mat_types[::3] = 7.0
+    odd.mat_types[1::5] = 0.5
+    cases = [(empty, 20, 10), (rtx.World(base.spheres, base.mat_types, base.mat_values, 10, 0), 9, 5),
+             (rtx.World(base.spheres, base.mat_types, base.mat_values, 0, 3), 9, 5), (odd, 31, 9),
+             (base, 1, 1)]
+    for world, w, h in cases:
+        frame = rtx.camera_look_at(w, h, aspect=max(w / h, 0.1))
+        img, _ = render_gpu(gpu_ctx, world, frame)
+        want, _ = oracle.render_rows(world, frame, np.arange(h))
+        assert_bits_equal(img, want, f"edge case n={world.count} spp={world.spp} depth={world.depth}")
+    img, _ = render_gpu(gpu_ctx, rtx.World(base.spheres, base.mat_types, base.mat_values, 10, 0),
+                        rtx.camera_look_at(4, 2))
+    assert np.isnan(img[..., :3]).all() and (img[..., 3] == 1).all()
+
+
+def test_determinism(gpu_ctx, rtx):
+    world = rtx.random_world(11, depth=50, spp=4)
+    frame = rtx.camera_look_at(320, 180)
+    a, _ = render_gpu(gpu_ctx, world, frame)
+    b, _ = render_gpu(gpu_ctx, world, frame)
+    assert_bits_equal(a, b, "two renders")
+
+
+# ---------------------------------------------------------------------------
+# row-tile partitions (the multi-GPU data path) on one device
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("nparts,tile_rows", [(2, 8), (3, 5), (8, 5), (8, 1), (5, 64)])
+def test_partitions_reassemble_bit_identical(gpu_ctx, rtx, nparts, tile_rows):
+    """Each part renders its interleaved row tiles into its own buffer; the
+    gathered buffers de-interleave (rtx_deinterleave_rows) into exactly the
+    single-device image — the R-rank frame is bit-identical for every R."""
+    import torch
+    W, H = 200, 117
+    world = rtx.random_world(11, depth=50, spp=3)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    full, _ = render_gpu(gpu_ctx, world, frame)
+    max_rows = rtx.part_rows(H, tile_rows, 0, nparts)
+    gathered = torch.zeros((nparts, max_rows, W, 4), dtype=torch.float32, device="cuda")
+    image = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # torch's fill runs on torch's stream, ours on the context stream
+    for p in range(nparts):
+        rows = rtx.part_rows(H, tile_rows, p, nparts)
+        assert rows == len(rtx.part_row_ids(H, tile_rows, p, nparts))
+        gpu_ctx.render_rows(tile_rows, p, nparts, gathered[p].data_ptr())
+    gpu_ctx.deinterleave(gathered.data_ptr(), W, H, tile_rows, nparts, image.data_ptr())
+    gpu_ctx.sync()
+    assert_bits_equal(image.cpu().numpy(), full, f"{nparts} parts x {tile_rows}-row tiles")
