@@ -8,7 +8,7 @@ PKG       := raytrace-we-gpu_amd
 SRC       := $(PKG)/csrc
 LIBDIR    := $(PKG)/lib
 BINDIR    := $(PKG)/bin
-HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function
 LIB       := $(LIBDIR)/librtx.so
 CLI       := $(BINDIR)/rtx_cli
 HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h

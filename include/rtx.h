@@ -156,6 +156,14 @@ RTX_API void *rtx_framebuffer(rtx_ctx *ctx);
  * never reads results back; this is the image-output contract (§8f-1). */
 RTX_API int rtx_download(rtx_ctx *ctx, float *host_rgba, size_t bytes);
 
+/* ---- device buffers (for callers without their own allocator) ----------
+ * Ordered on the context stream; copies are synchronous. d_ptr from
+ * rtx_alloc may be passed as d_out / d_gathered / d_image above. */
+RTX_API int rtx_alloc(rtx_ctx *ctx, size_t bytes, void **d_ptr);
+RTX_API int rtx_free(rtx_ctx *ctx, void *d_ptr);
+RTX_API int rtx_copy_to_host(rtx_ctx *ctx, void *host, const void *d_src, size_t bytes);
+RTX_API int rtx_copy_to_device(rtx_ctx *ctx, void *d_dst, const void *host, size_t bytes);
+
 /* ---- measurement ------------------------------------------------------ */
 RTX_API int rtx_stats_reset(rtx_ctx *ctx);
 /* Synchronises the stream, then reports counters since the last reset. */

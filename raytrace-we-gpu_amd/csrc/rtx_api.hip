@@ -141,7 +141,8 @@ int rtx_create(int hip_device, rtx_ctx **out) {
     }
     c->stream = c->own_stream;
     e = hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
@@ -204,11 +205,14 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     RTX_HIP(hipMalloc(&c->d_rad, cap * sizeof(float)));
     RTX_HIP(hipMalloc(&c->d_mtype, cap * sizeof(int)));
     RTX_HIP(hipMalloc(&c->d_mval, cap * sizeof(float4)));
+    // All copies on the context stream (a non-blocking stream does not
+    // order against the legacy null stream), then wait for them.
     if (n) {
-        RTX_HIP(hipMemcpy(c->d_sph, sph.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice));
-        RTX_HIP(hipMemcpy(c->d_rad, rad.data(), n * sizeof(float), hipMemcpyHostToDevice));
-        RTX_HIP(hipMemcpy(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice));
-        RTX_HIP(hipMemcpy(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        RTX_HIP(hipMemcpyAsync(c->d_sph, sph.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_rad, rad.data(), n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipStreamSynchronize(c->stream));
     }
     if (c->n != n) c->n_changed = true;
     c->n = n;
@@ -337,8 +341,8 @@ int rtx_download(rtx_ctx *c, float *host, size_t bytes) {
         return fail(RTX_ERR_INVALID, "rtx_download: bytes != width*height*16");
     int rc = set_device(c);
     if (rc) return rc;
+    RTX_HIP(hipMemcpyAsync(host, c->d_fb, bytes, hipMemcpyDeviceToHost, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
-    RTX_HIP(hipMemcpy(host, c->d_fb, bytes, hipMemcpyDeviceToHost));
     return RTX_OK;
 }
 
@@ -346,8 +350,8 @@ int rtx_stats_reset(rtx_ctx *c) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_stats_reset: null ctx");
     int rc = set_device(c);
     if (rc) return rc;
+    RTX_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
-    RTX_HIP(hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)));
     c->events_used = 0;
     c->samples = 0;
     c->launches = 0;
@@ -362,7 +366,8 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     if (rc) return rc;
     RTX_HIP(hipStreamSynchronize(c->stream));
     unsigned long long h[4];
-    RTX_HIP(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+    RTX_HIP(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    RTX_HIP(hipStreamSynchronize(c->stream));
     double ms = 0.0;
     for (size_t i = 0; i < c->events_used; ++i) {
         float t = 0.0f;
@@ -377,6 +382,47 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     return RTX_OK;
 }
 
+int rtx_alloc(rtx_ctx *c, size_t bytes, void **d_ptr) {
+    if (!c || !d_ptr) return fail(RTX_ERR_INVALID, "rtx_alloc: null argument");
+    *d_ptr = nullptr;
+    int rc = set_device(c);
+    if (rc) return rc;
+    hipError_t e = hipMalloc(d_ptr, bytes ? bytes : 1);
+    if (e == hipErrorOutOfMemory) return fail(RTX_ERR_NOMEM, "rtx_alloc: out of device memory");
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    return RTX_OK;
+}
+
+int rtx_free(rtx_ctx *c, void *d_ptr) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_free: null ctx");
+    if (!d_ptr) return RTX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    RTX_HIP(hipFree(d_ptr));
+    return RTX_OK;
+}
+
+int rtx_copy_to_host(rtx_ctx *c, void *host, const void *d_src, size_t bytes) {
+    if (!c || ((!host || !d_src) && bytes)) return fail(RTX_ERR_INVALID, "rtx_copy_to_host: null argument");
+    if (!bytes) return RTX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipMemcpyAsync(host, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+int rtx_copy_to_device(rtx_ctx *c, void *d_dst, const void *host, size_t bytes) {
+    if (!c || ((!host || !d_dst) && bytes)) return fail(RTX_ERR_INVALID, "rtx_copy_to_device: null argument");
+    if (!bytes) return RTX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    RTX_HIP(hipMemcpyAsync(d_dst, host, bytes, hipMemcpyHostToDevice, c->stream));
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
 int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_min, float t_max,
                         float *out) {
     if (!c || (nrays && (!rays || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_hit_world: null argument");
@@ -387,10 +433,10 @@ int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_m
     float *d_rays = nullptr, *d_out = nullptr;
     RTX_HIP(hipMalloc(&d_rays, (size_t)nrays * 6 * sizeof(float)));
     hipError_t e = hipMalloc(&d_out, (size_t)nrays * 10 * sizeof(float));
-    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, (size_t)nrays * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rays, rays, (size_t)nrays * 6 * sizeof(float), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = rtx::launch_debug_hit_world(scene_of(c), d_rays, nrays, t_min, t_max, d_out, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, (size_t)nrays * 10 * sizeof(float), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e == hipSuccess) e = hipMemcpy(out, d_out, (size_t)nrays * 10 * sizeof(float), hipMemcpyDeviceToHost);
     (void)hipFree(d_rays);
     (void)hipFree(d_out);
     if (e != hipSuccess) return hip_fail(e, "rtx_debug_hit_world");
@@ -408,13 +454,13 @@ int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint3
     RTX_HIP(hipMalloc(&d0, (size_t)n * sizeof(float)));
     hipError_t e = hipMalloc(&dout, outn * sizeof(float));
     if (e == hipSuccess && in1) e = hipMalloc(&d1, (size_t)n * sizeof(float));
-    if (e == hipSuccess) e = hipMemcpy(d0, in0, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
-    if (e == hipSuccess && in1) e = hipMemcpy(d1, in1, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(dout, 0, outn * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpyAsync(d0, in0, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && in1) e = hipMemcpyAsync(d1, in1, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dout, 0, outn * sizeof(float), c->stream);
     if (e == hipSuccess) e = rtx::launch_debug_math(fn, d0, d1, n, dout, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     const size_t copy_n = (fn >= RTX_FN_HASH1) ? outn : (size_t)n;
-    if (e == hipSuccess) e = hipMemcpy(out, dout, copy_n * sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, copy_n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d0);
     (void)hipFree(d1);
     (void)hipFree(dout);

@@ -86,6 +86,10 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_sync": (C.c_int, [ctx]),
         "rtx_framebuffer": (vp, [ctx]),
         "rtx_download": (C.c_int, [ctx, f, C.c_size_t]),
+        "rtx_alloc": (C.c_int, [ctx, C.c_size_t, C.POINTER(C.c_void_p)]),
+        "rtx_free": (C.c_int, [ctx, vp]),
+        "rtx_copy_to_host": (C.c_int, [ctx, vp, vp, C.c_size_t]),
+        "rtx_copy_to_device": (C.c_int, [ctx, vp, vp, C.c_size_t]),
         "rtx_stats_reset": (C.c_int, [ctx]),
         "rtx_get_stats": (C.c_int, [ctx, C.POINTER(rtx_stats)]),
         "rtx_scene_random_world": (C.c_int, [i32, u32, f, f, f, C.POINTER(u32)]),
@@ -281,6 +285,9 @@ class Context:
         self.render()
         return self.download()
 
+    def alloc(self, shape, dtype=np.float32) -> "DeviceArray":
+        return DeviceArray(self, shape, dtype)
+
     def stats_reset(self):
         _check(self._lib.rtx_stats_reset(self._h), "rtx_stats_reset")
 
@@ -305,3 +312,37 @@ class Context:
                                         _fptr(b) if b is not None else None, a.size, _fptr(out)),
                "rtx_debug_math")
         return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
+
+
+class DeviceArray:
+    """Device buffer owned by a Context (rtx_alloc/rtx_free), no torch needed."""
+
+    def __init__(self, ctx: Context, shape, dtype=np.float32):
+        self.ctx, self.shape, self.dtype = ctx, tuple(shape), np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = C.c_void_p()
+        _check(ctx._lib.rtx_alloc(ctx._h, self.nbytes, C.byref(p)), "rtx_alloc")
+        self.ptr = int(p.value)
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        _check(self.ctx._lib.rtx_copy_to_host(self.ctx._h, out.ctypes.data, C.c_void_p(self.ptr),
+                                              self.nbytes), "rtx_copy_to_host")
+        return out
+
+    def upload(self, a: np.ndarray):
+        a = np.ascontiguousarray(a, self.dtype)
+        assert a.nbytes == self.nbytes
+        _check(self.ctx._lib.rtx_copy_to_device(self.ctx._h, C.c_void_p(self.ptr), a.ctypes.data,
+                                                self.nbytes), "rtx_copy_to_device")
+
+    def free(self):
+        if self.ptr and self.ctx._h:
+            _check(self.ctx._lib.rtx_free(self.ctx._h, C.c_void_p(self.ptr)), "rtx_free")
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

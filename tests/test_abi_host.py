@@ -1,0 +1,97 @@
+"""C-ABI surface and host logic (CPU only, no GPU compute calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    """Every RTX_API function declared in include/*.h."""
+    names = set()
+    for h in os.listdir(os.path.join(ROOT, "include")):
+        if not h.endswith(".h"):
+            continue
+        text = open(os.path.join(ROOT, "include", h)).read()
+        for m in re.finditer(r"RTX_API\s+[^;(]*?\b(rtx_\w+)\s*\(", text):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_header_declares_boundary():
+    names = declared_symbols()
+    for must in ("rtx_create", "rtx_destroy", "rtx_upload_world", "rtx_set_frame", "rtx_render_rows",
+                 "rtx_sync", "rtx_download", "rtx_last_error", "rtx_deinterleave_rows"):
+        assert must in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol(rtx):
+    lib = rtx.load_library()
+    missing = [n for n in declared_symbols() if not hasattr(lib, n)]
+    assert not missing, f"librtx.so lacks {missing}"
+    out = subprocess.run(["nm", "-D", "--defined-only", rtx.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert set(declared_symbols()) <= exported
+    # nothing but the C-ABI leaks out (no C++ mangled product symbols)
+    assert not [s for s in exported if s.startswith("_ZN3rtx")]
+
+
+def test_library_built_for_gfx950(rtx):
+    """The embedded HIP fat binary carries a gfx950 (MI355X) code object."""
+    blob = open(rtx.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_version_and_error_paths(rtx):
+    lib = rtx.load_library()
+    assert lib.rtx_version() == 100
+    # null arguments are rejected without touching the GPU
+    assert lib.rtx_upload_world(None, None) == -1
+    assert b"null" in lib.rtx_last_error()
+    assert lib.rtx_set_frame(None, None) == -1
+    assert lib.rtx_render_rows(None, 1, 0, 1, None) == -1
+    assert lib.rtx_sync(None) == -1
+    assert lib.rtx_get_stats(None, None) == -1
+    f = rtx.rtx_frame()
+    assert lib.rtx_camera_look_at(None, None, None, 20.0, 1.0, 0.0, 0.0, 4, 4, C.byref(f)) == -1
+
+
+@pytest.mark.parametrize("H,T,R", [(1080, 5, 8), (1080, 5, 1), (117, 8, 3), (117, 64, 5),
+                                   (10, 3, 8), (1, 1, 2), (2160, 8, 8), (1081, 5, 8)])
+def test_part_rows_matches_definition(rtx, H, T, R):
+    total = 0
+    for p in range(R):
+        ids = rtx.part_row_ids(H, T, p, R)
+        assert rtx.part_rows(H, T, p, R) == len(ids)
+        total += len(ids)
+    assert total == H
+    # part 0 is the largest part (used to size equal gather buffers)
+    assert rtx.part_rows(H, T, 0, R) == max(rtx.part_rows(H, T, p, R) for p in range(R))
+    assert rtx.part_rows(H, T, R, R) == 0 and rtx.part_rows(H, 0, 0, R) == 0
+
+
+def deinterleave_np(gathered, H, T, R):
+    """Numpy statement of rtx_deinterleave_rows (rtx_kernels.hip k_deinterleave)."""
+    W = gathered.shape[2]
+    img = np.empty((H, W) + gathered.shape[3:], gathered.dtype)
+    for y in range(H):
+        tile = y // T
+        img[y] = gathered[tile % R, (tile // R) * T + (y - tile * T)]
+    return img
+
+
+@pytest.mark.parametrize("H,T,R", [(1080, 5, 8), (117, 8, 3), (31, 4, 5)])
+def test_deinterleave_inverts_partition(rtx, H, T, R):
+    W = 3
+    img = np.random.default_rng(H).normal(size=(H, W)).astype(np.float32)
+    maxr = rtx.part_rows(H, T, 0, R)
+    g = np.zeros((R, maxr, W), np.float32)
+    for p in range(R):
+        ids = rtx.part_row_ids(H, T, p, R)
+        g[p, :len(ids)] = img[ids]
+    np.testing.assert_array_equal(deinterleave_np(g, H, T, R), img)

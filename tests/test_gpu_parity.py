@@ -222,20 +222,26 @@ def test_determinism(gpu_ctx, rtx):
 def test_partitions_reassemble_bit_identical(gpu_ctx, rtx, nparts, tile_rows):
     """Each part renders its interleaved row tiles into its own buffer; the
     gathered buffers de-interleave (rtx_deinterleave_rows) into exactly the
-    single-device image — the R-rank frame is bit-identical for every R."""
-    import torch
+    single-device image — the R-rank frame is bit-identical for every R.
+    (Device buffers come from rtx_alloc: no second HIP runtime via torch.)"""
     W, H = 200, 117
     world = rtx.random_world(11, depth=50, spp=3)
     frame = rtx.camera_look_at(W, H, aspect=W / H)
     full, _ = render_gpu(gpu_ctx, world, frame)
     max_rows = rtx.part_rows(H, tile_rows, 0, nparts)
-    gathered = torch.zeros((nparts, max_rows, W, 4), dtype=torch.float32, device="cuda")
-    image = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
-    torch.cuda.synchronize()  # torch's fill runs on torch's stream, ours on the context stream
+    gathered = gpu_ctx.alloc((nparts, max_rows, W, 4))
+    gathered.upload(np.zeros((nparts, max_rows, W, 4), np.float32))
+    image = gpu_ctx.alloc((H, W, 4))
+    part_bytes = max_rows * W * 16
     for p in range(nparts):
         rows = rtx.part_rows(H, tile_rows, p, nparts)
         assert rows == len(rtx.part_row_ids(H, tile_rows, p, nparts))
-        gpu_ctx.render_rows(tile_rows, p, nparts, gathered[p].data_ptr())
-    gpu_ctx.deinterleave(gathered.data_ptr(), W, H, tile_rows, nparts, image.data_ptr())
-    gpu_ctx.sync()
-    assert_bits_equal(image.cpu().numpy(), full, f"{nparts} parts x {tile_rows}-row tiles")
+        gpu_ctx.render_rows(tile_rows, p, nparts, gathered.ptr + p * part_bytes)
+    g = gathered.numpy()
+    for p in range(nparts):
+        ids = rtx.part_row_ids(H, tile_rows, p, nparts)
+        assert_bits_equal(g[p, :len(ids)], full[ids], f"part {p} rows")
+    gpu_ctx.deinterleave(gathered.ptr, W, H, tile_rows, nparts, image.ptr)
+    assert_bits_equal(image.numpy(), full, f"{nparts} parts x {tile_rows}-row tiles")
+    gathered.free()
+    image.free()

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU-box session: every GPU step under its own timeout; a crash,
+# abort, or timeout (exit >= 124 or signal) ends the script there. Test
+# failures (exit 1/2: pytest failures, Python exceptions) do not stop the
+# later measurement steps.
+# Usage: tools/gpu_session.sh TAG [steps...]   steps: ubench tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=${*:-ubench tests smoke bench prof}
+fatal() { echo "STOP: step $1 exited $2" | tee -a "$OUT/session.log"; exit "$2"; }
+run() {  # name timeout cmd...
+    local name=$1 to=$2; shift 2
+    echo "== $name: $*" >> "$OUT/session.log"
+    local t0=$(date +%s)
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a "$OUT/session.log"
+    # >= 124: timeout (124/137) or killed by a signal (134 abort, 139 segv): stop.
+    if [ $rc -ge 124 ]; then fatal "$name" $rc; fi
+    return 0
+}
+for s in $STEPS; do
+  case $s in
+    ubench) run ubench 120 ./tools/ubench_valu ;;
+    tests)  run tests 900 python -m pytest tests -m gpu -q -rA ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+                python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
+    pmc)    for c in FETCH_SIZE WRITE_SIZE; do
+              run pmc_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
+                  python3 bench.py --probe ; done ;;
+  esac
+done
+echo "session done" >> "$OUT/session.log"
