@@ -42,3 +42,25 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle asm clean
+
+# Kernel variants for A/B timing (tools/variant_bench.py): same sources,
+# different compile-time choices. Not used by the product path.
+VARIANTS := lds_b4 lds_b8 scalar_b4 scalar_b8 lds_b4_noslp scalar_b8_noslp
+VFLAGS_lds_b4          := -DRTX_SRC=0 -DRTX_BATCH=4
+VFLAGS_lds_b8          := -DRTX_SRC=0 -DRTX_BATCH=8
+VFLAGS_scalar_b4       := -DRTX_SRC=1 -DRTX_BATCH=4
+VFLAGS_scalar_b8       := -DRTX_SRC=1 -DRTX_BATCH=8
+VFLAGS_lds_b4_noslp    := -DRTX_SRC=0 -DRTX_BATCH=4 -fno-slp-vectorize
+VFLAGS_scalar_b8_noslp := -DRTX_SRC=1 -DRTX_BATCH=8 -fno-slp-vectorize
+VDIR := $(LIBDIR)/variants
+
+variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
+
+$(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS)
+	mkdir -p $(VDIR)/$*
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$*/k.o
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(VDIR)/$*/k.o $(VDIR)/$*/a.o $(VDIR)/$*/h.o
+
+.PHONY: variants

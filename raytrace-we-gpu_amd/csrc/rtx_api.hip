@@ -46,8 +46,8 @@ struct rtx_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // own_stream or an external one
     // scene (device)
-    float4 *d_sph = nullptr;
-    float *d_rad = nullptr;
+    float *d_soa = nullptr;
+    float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
     uint32_t n = 0, n_pad = 0, depth = 0, spp = 0;
@@ -75,12 +75,12 @@ int set_device(rtx_ctx *c) {
 }
 
 void free_world(rtx_ctx *c) {
-    (void)hipFree(c->d_sph);
-    (void)hipFree(c->d_rad);
+    (void)hipFree(c->d_soa);
+    (void)hipFree(c->d_cen);
     (void)hipFree(c->d_mtype);
     (void)hipFree(c->d_mval);
-    c->d_sph = nullptr;
-    c->d_rad = nullptr;
+    c->d_soa = nullptr;
+    c->d_cen = nullptr;
     c->d_mtype = nullptr;
     c->d_mval = nullptr;
     c->have_world = false;
@@ -88,8 +88,8 @@ void free_world(rtx_ctx *c) {
 
 rtx::KScene scene_of(const rtx_ctx *c) {
     rtx::KScene s;
-    s.sph = c->d_sph;
-    s.rad = c->d_rad;
+    s.soa = c->d_soa;
+    s.cen = c->d_cen;
     s.mtype = c->d_mtype;
     s.mval = c->d_mval;
     s.n = c->n;
@@ -182,14 +182,22 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (rc) return rc;
     const uint32_t n = w->count;
     const uint32_t n_pad = (n + rtx::kPad - 1) / rtx::kPad * rtx::kPad;
-    std::vector<float4> sph(n_pad), mval(n);
-    std::vector<float> rad(n);
+    std::vector<float> soa(4 * (size_t)n_pad);
+    std::vector<float4> cen(n), mval(n);
     std::vector<int> mtype(n);
+    for (uint32_t i = 0; i < n_pad; ++i) {
+        // padding: copies of sphere n-1 (see rtx::KScene)
+        const uint32_t k = i < n ? i : n - 1;
+        const float r = w->spheres[4 * k + 3];
+        float *blk = &soa[32 * (size_t)(i / 8)];
+        blk[i % 8] = w->spheres[4 * k + 0];
+        blk[8 + i % 8] = w->spheres[4 * k + 1];
+        blk[16 + i % 8] = w->spheres[4 * k + 2];
+        blk[24 + i % 8] = -(r * r);
+    }
     for (uint32_t i = 0; i < n; ++i) {
-        const float r = w->spheres[4 * i + 3];
-        sph[i] = make_float4(w->spheres[4 * i + 0], w->spheres[4 * i + 1], w->spheres[4 * i + 2],
-                             -(r * r));
-        rad[i] = r;
+        cen[i] = make_float4(w->spheres[4 * i + 0], w->spheres[4 * i + 1], w->spheres[4 * i + 2],
+                             w->spheres[4 * i + 3]);
         // The shader compares the float code with 0, 1, 2 (:209,219,229);
         // anything else does not scatter.
         const float t = w->mat_types[i];
@@ -197,19 +205,18 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         mval[i] = make_float4(w->mat_values[4 * i + 0], w->mat_values[4 * i + 1],
                               w->mat_values[4 * i + 2], w->mat_values[4 * i + 3]);
     }
-    for (uint32_t i = n; i < n_pad; ++i) sph[i] = sph[n - 1];  // see rtx::KScene
     RTX_HIP(hipStreamSynchronize(c->stream));
     free_world(c);
     const size_t cap = n ? n : 1;
-    RTX_HIP(hipMalloc(&c->d_sph, (n_pad ? n_pad : 1) * sizeof(float4)));
-    RTX_HIP(hipMalloc(&c->d_rad, cap * sizeof(float)));
+    RTX_HIP(hipMalloc(&c->d_soa, (n_pad ? 4 * (size_t)n_pad : 4) * sizeof(float)));
+    RTX_HIP(hipMalloc(&c->d_cen, cap * sizeof(float4)));
     RTX_HIP(hipMalloc(&c->d_mtype, cap * sizeof(int)));
     RTX_HIP(hipMalloc(&c->d_mval, cap * sizeof(float4)));
     // All copies on the context stream (a non-blocking stream does not
     // order against the legacy null stream), then wait for them.
     if (n) {
-        RTX_HIP(hipMemcpyAsync(c->d_sph, sph.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-        RTX_HIP(hipMemcpyAsync(c->d_rad, rad.data(), n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_soa, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_cen, cen.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipStreamSynchronize(c->stream));

@@ -7,23 +7,25 @@
 
 namespace rtx {
 
-// Device scene layout (structure of arrays, all in HBM, read-only):
-//   sph   float4[n]  center.xyz, -(radius*radius)  — streamed by every ray segment
-//   rad   float [n]  radius                  — read once per hit (normal)
+// Device scene layout (all in HBM, read-only):
+//   soa   float[n_pad*4]  AoSoA-8 blocks of 8 spheres, 128 B each:
+//                         cx[8] cy[8] cz[8] -(r*r)[8] — streamed by every
+//                         ray segment (LDS broadcast or scalar loads)
+//   cen   float4[n]  center.xyz, radius  — read once per hit (normal)
 //   mtype int   [n]  material code 0/1/2, 3 = "no scatter"
 //   mval  float4[n]  albedo.rgb, fuzz-or-ir
-// `sph` is padded to n_pad = roundup(n, kPad) entries with copies of sphere
+// `soa` is padded to n_pad = roundup(n, kPad) spheres with copies of sphere
 // n-1; a padded copy can only win where sphere n-1 itself would (same data,
 // later index wins ties), so kernels clamp the winning index to n-1.
 struct KScene {
-    const float4 *sph;
-    const float *rad;
+    const float *soa;
+    const float4 *cen;
     const int *mtype;
     const float4 *mval;
     uint32_t n, n_pad;
 };
 
-constexpr uint32_t kPad = 8;
+constexpr uint32_t kPad = 8;  // spheres per AoSoA block
 
 // Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
 struct KParams {
@@ -38,8 +40,8 @@ struct KParams {
     float img_w, img_h;
 };
 
-// Spheres kept resident in LDS up to this count (16 B each); larger scenes
-// are streamed through LDS in chunks of kChunk spheres.
+// LDS variant: spheres kept resident in LDS up to this count (16 B each);
+// larger scenes are streamed through LDS in chunks of kChunk spheres.
 constexpr uint32_t kResidentMax = 4096;  // 64 KiB
 constexpr uint32_t kChunk = 1024;        // 16 KiB
 constexpr uint32_t kBlock = 256;         // 4 waves

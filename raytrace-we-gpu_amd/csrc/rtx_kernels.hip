@@ -13,9 +13,12 @@
 //    iteration instead of idling while the longest path of the wave
 //    finishes;
 //  * hit_world is a linear closest-hit scan over the sphere array in index
-//    order (Hittable_list.cpp:3-20 / ShaderCompute.hlsl:188-205), spheres
-//    read from LDS by wave-uniform (broadcast) ds_read_b128: resident for
-//    n <= kResidentMax, streamed in kChunk tiles otherwise;
+//    order (Hittable_list.cpp:3-20 / ShaderCompute.hlsl:188-205) over an
+//    AoSoA-8 layout, so packed-fp32 pairs (v_pk_fma_f32) come straight from
+//    consecutive registers. Sphere data is wave-uniform; RTX_SRC selects
+//    where it is read from: 0 = LDS by broadcast ds_read_b128 (resident for
+//    n <= kResidentMax, streamed in kChunk tiles otherwise), 1 = scalar
+//    loads (s_load into SGPRs through the scalar cache / L2);
 //  * the quadratic's root/sqrt work sits behind the per-sphere "disc >= 0"
 //    branch, so a wave skips it when no lane's ray line meets the sphere
 //    (the wave-level early-out on all-miss);
@@ -58,24 +61,18 @@ __device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_
 // a = |d|^2 (Sphere.cpp:8; HLSL length(d)*length(d), :160), fma form.
 __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y, d.y, d.x * d.x)); }
 
-// One ray against spheres [0, n) of `sph` (global indices base + i), in
-// index order. `best` is closest_so_far (t_max shrinks on every accepted
-// hit, :196-200); strict rejection `root < t_min || t_max < root` (:171,174)
-// lets a later sphere win an exact tie. Returns the winning index or `idx`.
-//
-// Per sphere (DESIGN.md §4, "hit_sphere"): oc = o - c; hb = oc.d;
-// cc = |oc|^2 - r^2; disc = hb^2 - a*cc; NaN disc falls through like the
-// reference's `if (d < 0) return false`.
-__device__ __forceinline__ float sphere_disc(const float4 s, f3 o, f3 d, float a, float &hb) {
-    const float ocx = o.x - s.x;
-    const float ocy = o.y - s.y;
-    const float ocz = o.z - s.z;
-    hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-    const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, s.w)));  // s.w = -r^2
-    return fmaf(hb, hb, -(a * cc));
-}
+#ifndef RTX_SRC
+#define RTX_SRC 0
+#endif
+#ifndef RTX_BATCH
+#define RTX_BATCH 4
+#endif
+static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
+
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
-// the near one is outside [t_min, best] (Sphere.cpp:15-24).
+// the near one is outside [t_min, best] (Sphere.cpp:15-24); strict
+// rejection `root < t_min || t_max < root` (ShaderCompute.hlsl:171,174)
+// lets a later sphere win an exact tie.
 __device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, float t_min,
                                              float &best, int &idx, int i) {
     const float sq = sqrtf(disc);
@@ -90,37 +87,57 @@ __device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, 
         idx = i;
     }
 }
-// n must be a multiple of kPad (the device array is padded with copies of
-// the last sphere; callers clamp the index to count-1, see pad_scene).
-// Four spheres per step: their LDS reads issue together, and one branch
-// skips all four when every lane's disc < 0 (wave-level all-miss early out).
-__device__ __forceinline__ int hit_range(const float4 *__restrict__ sph, uint32_t n,
-                                         uint32_t base, f3 o, f3 d, float a, float inv_a,
-                                         float t_min, float &best, int idx) {
-    for (uint32_t i = 0; i < n; i += 4) {
-        const float4 s0 = sph[i + 0];
-        const float4 s1 = sph[i + 1];
-        const float4 s2 = sph[i + 2];
-        const float4 s3 = sph[i + 3];
-        float hb0, hb1, hb2, hb3;
-        const float d0 = sphere_disc(s0, o, d, a, hb0);
-        const float d1 = sphere_disc(s1, o, d, a, hb1);
-        const float d2 = sphere_disc(s2, o, d, a, hb2);
-        const float d3 = sphere_disc(s3, o, d, a, hb3);
-        // Wave-uniform: skip the four root computations when no lane's ray
-        // line meets any of the four spheres.
-        const uint64_t any = __ballot(!(d0 < 0.0f)) | __ballot(!(d1 < 0.0f)) |
-                             __ballot(!(d2 < 0.0f)) | __ballot(!(d3 < 0.0f));
-        if (any != 0ull) {
-            const int g = (int)(base + i);
-            if (!(d0 < 0.0f)) sphere_roots(hb0, d0, inv_a, t_min, best, idx, g + 0);
-            if (!(d1 < 0.0f)) sphere_roots(hb1, d1, inv_a, t_min, best, idx, g + 1);
-            if (!(d2 < 0.0f)) sphere_roots(hb2, d2, inv_a, t_min, best, idx, g + 2);
-            if (!(d3 < 0.0f)) sphere_roots(hb3, d3, inv_a, t_min, best, idx, g + 3);
+
+// One ray against `nblk` AoSoA-8 blocks (global sphere index of block b's
+// first sphere: 8 * (blk0 + b)), in index order; `best` is closest_so_far
+// (t_max shrinks on every accepted hit, :196-200). Returns the winning
+// index or `idx`.
+//
+// Per sphere (DESIGN.md §4, "hit_sphere"): oc = o - c; hb = oc.d;
+// cc = |oc|^2 - r^2; disc = hb^2 - a*cc. NaN disc falls through like the
+// reference's `if (d < 0) return false`. RTX_BATCH spheres per step: their
+// reads issue together and one wave-uniform branch skips the root work
+// when no lane's ray line meets any of them (all-miss early out).
+template <typename Ptr>
+__device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d,
+                                          float a, float inv_a, float t_min, float &best,
+                                          int idx) {
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const Ptr blk = soa + 32 * b;
+#pragma unroll
+        for (int h = 0; h < 8; h += RTX_BATCH) {
+            float cx[RTX_BATCH], cy[RTX_BATCH], cz[RTX_BATCH], nr2[RTX_BATCH];
+#pragma unroll
+            for (int q = 0; q < RTX_BATCH; ++q) {
+                cx[q] = blk[h + q];
+                cy[q] = blk[8 + h + q];
+                cz[q] = blk[16 + h + q];
+                nr2[q] = blk[24 + h + q];
+            }
+            float hb[RTX_BATCH], disc[RTX_BATCH];
+            uint64_t any = 0;
+#pragma unroll
+            for (int k = 0; k < RTX_BATCH; ++k) {
+                const float ocx = o.x - cx[k];
+                const float ocy = o.y - cy[k];
+                const float ocz = o.z - cz[k];
+                hb[k] = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+                const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, nr2[k])));
+                disc[k] = fmaf(hb[k], hb[k], -(a * cc));
+                any |= __ballot(!(disc[k] < 0.0f));
+            }
+            if (any != 0ull) {
+                const int g = (int)(8 * (blk0 + b) + h);
+#pragma unroll
+                for (int k = 0; k < RTX_BATCH; ++k)
+                    if (!(disc[k] < 0.0f)) sphere_roots(hb[k], disc[k], inv_a, t_min, best, idx, g + k);
+            }
         }
     }
     return idx;
 }
+
+typedef const __attribute__((address_space(4))) float *cfloat_p;  // constant AS: scalar loads
 
 // Lane state of one pixel's path tracer.
 struct Lane {
@@ -166,9 +183,9 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, uint32_t
     bool ended = false;
     if (hit >= 0) {
         const KScene &S = P.scene;
-        const float4 sc = S.sph[hit];
+        const float4 sc = S.cen[hit];
         const f3 p = L.o + t * L.d;                    // Ray::at, Ray.h:16-19
-        const float inv_r = 1.0f / S.rad[hit];         // Vec3 operator/, Vec3.h:83-86
+        const float inv_r = 1.0f / sc.w;               // Vec3 operator/, Vec3.h:83-86
         f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));  // Sphere.cpp:28
         const bool ff = dot3(L.d, nrm) < 0.0f;         // set_face_normal, :143-150
         if (!ff) nrm = -nrm;
@@ -279,12 +296,14 @@ __device__ __forceinline__ void init_lane(const KParams &P, const Frame &F, uint
     if (L.active) begin_sample(P, F, x, y, L);
 }
 
-// Scene resident in LDS (n <= kResidentMax): waves run independently.
+// Sphere blocks resident in LDS (n_pad <= kResidentMax): waves run independently.
 __global__ void __launch_bounds__(kBlock) k_render_resident(const KParams P) {
-    extern __shared__ float4 s_sph[];
-    const uint32_t n = P.scene.n_pad;
+    extern __shared__ float4 s_blk4[];
+    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
+    const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) s_sph[i] = P.scene.sph[i];
+    const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
+    for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kBlock) s_blk4[i] = g4[i];
     __syncthreads();
 
     const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
@@ -298,19 +317,21 @@ __global__ void __launch_bounds__(kBlock) k_render_resident(const KParams P) {
     while (__ballot(L.active) != 0ull) {
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
-            const int hit = hit_range(s_sph, n, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+            const int hit = hit_blocks(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
             shade(P, F, x, y, L, min(hit, last), best);
         }
     }
     finish(P, gid, L, valid);
 }
 
-// Large scenes: every ray segment streams the sphere array through LDS in
-// kChunk-sphere tiles shared by the block's 4 waves (block-synchronous).
+// Large scenes (LDS variant): every ray segment streams the sphere blocks
+// through LDS in kChunk-sphere tiles shared by the block's 4 waves.
 __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
-    extern __shared__ float4 s_sph[];
-    const uint32_t n = P.scene.n_pad;
+    extern __shared__ float4 s_blk4[];
+    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
+    const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
+    const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
     const bool valid = gid < P.rows_local * P.width;
     uint32_t x = 0, y = 0;
@@ -319,17 +340,43 @@ __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
     Lane L;
     init_lane(P, F, x, y, valid, L);
 
+    constexpr uint32_t kChunkBlk = kChunk / 8;
     while (__syncthreads_or(L.active ? 1 : 0)) {
         float best = __uint_as_float(0x7f800000u);
         int hit = -1;
-        for (uint32_t base = 0; base < n; base += kChunk) {
-            const uint32_t cnt = min(kChunk, n - base);
+        for (uint32_t b0 = 0; b0 < nblk; b0 += kChunkBlk) {
+            const uint32_t cnt = min(kChunkBlk, nblk - b0);
             __syncthreads();
-            for (uint32_t i = threadIdx.x; i < cnt; i += kBlock) s_sph[i] = P.scene.sph[base + i];
+            for (uint32_t i = threadIdx.x; i < 8 * cnt; i += kBlock) s_blk4[i] = g4[8 * b0 + i];
             __syncthreads();
-            if (L.active) hit = hit_range(s_sph, cnt, base, L.o, L.d, L.a, L.inv_a, kTMin, best, hit);
+            if (L.active) hit = hit_blocks(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit);
         }
         if (L.active) shade(P, F, x, y, L, min(hit, last), best);
+    }
+    finish(P, gid, L, valid);
+}
+
+// Scalar variant: sphere blocks read by wave-uniform scalar loads straight
+// from global memory (constant address space -> s_load into SGPRs); no LDS,
+// no block synchronisation, any n.
+__global__ void __launch_bounds__(kBlock) k_render_scalar(const KParams P) {
+    const uint32_t nblk = P.scene.n_pad / 8;
+    const int last = (int)P.scene.n - 1;
+    const cfloat_p soa = (cfloat_p)P.scene.soa;
+    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = gid < P.rows_local * P.width;
+    uint32_t x = 0, y = 0;
+    if (valid) lane_pixel(P, gid, x, y);
+    const Frame F = load_frame(P);
+    Lane L;
+    init_lane(P, F, x, y, valid, L);
+
+    while (__ballot(L.active) != 0ull) {
+        if (L.active) {
+            float best = __uint_as_float(0x7f800000u);
+            const int hit = hit_blocks(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+            shade(P, F, x, y, L, min(hit, last), best);
+        }
     }
     finish(P, gid, L, valid);
 }
@@ -359,16 +406,17 @@ __global__ void __launch_bounds__(kBlock) k_debug_hit_world(const KScene S, cons
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx = min(hit_range(S.sph, S.n_pad, 0, o, d, a, inv_a, t_min, best, -1), (int)S.n - 1);
+    const int idx =
+        min(hit_blocks((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1), (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
         for (int k = 0; k < 10; ++k) r[k] = 0.0f;
         r[9] = -1.0f;
         return;
     }
-    const float4 sc = S.sph[idx];
+    const float4 sc = S.cen[idx];
     const f3 p = o + best * d;
-    const float inv_r = 1.0f / S.rad[idx];
+    const float inv_r = 1.0f / sc.w;
     f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));
     const bool ff = dot3(d, nrm) < 0.0f;
     if (!ff) nrm = -nrm;
@@ -412,7 +460,9 @@ hipError_t launch_render(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t blocks = ceil_div(lanes, kBlock);
-    if (p.scene.n_pad <= kResidentMax) {
+    if (RTX_SRC == 1) {
+        hipLaunchKernelGGL(k_render_scalar, dim3(blocks), dim3(kBlock), 0, stream, p);
+    } else if (p.scene.n_pad <= kResidentMax) {
         const size_t lds = (size_t)(p.scene.n_pad ? p.scene.n_pad : 1) * sizeof(float4);
         hipLaunchKernelGGL(k_render_resident, dim3(blocks), dim3(kBlock), lds, stream, p);
     } else {

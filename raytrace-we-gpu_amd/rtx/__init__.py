@@ -115,9 +115,9 @@ def _fptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
-def _check(rc: int, what: str):
+def _check(rc: int, what: str, lib: Optional[C.CDLL] = None):
     if rc != RTX_OK:
-        msg = load_library().rtx_last_error().decode(errors="replace")
+        msg = (lib or load_library()).rtx_last_error().decode(errors="replace")
         raise RtxError(f"{what} failed ({rc}): {msg}")
 
 
@@ -216,8 +216,9 @@ def device_count() -> int:
 class Context:
     """One HIP device's renderer (~ CDx11Base::Initialize .. Terminate)."""
 
-    def __init__(self, device: int = 0, stream: Optional[int] = None):
-        self._lib = load_library()
+    def __init__(self, device: int = 0, stream: Optional[int] = None,
+                 lib: Optional[C.CDLL] = None):
+        self._lib = lib or load_library()
         h = C.c_void_p()
         _check(self._lib.rtx_create(device, C.byref(h)), "rtx_create")
         self._h = h
