@@ -45,13 +45,15 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := lds_b4 lds_b8 scalar_b4 scalar_b8 lds_b4_noslp scalar_b8_noslp
-VFLAGS_lds_b4          := -DRTX_SRC=0 -DRTX_BATCH=4
-VFLAGS_lds_b8          := -DRTX_SRC=0 -DRTX_BATCH=8
-VFLAGS_scalar_b4       := -DRTX_SRC=1 -DRTX_BATCH=4
-VFLAGS_scalar_b8       := -DRTX_SRC=1 -DRTX_BATCH=8
-VFLAGS_lds_b4_noslp    := -DRTX_SRC=0 -DRTX_BATCH=4 -fno-slp-vectorize
-VFLAGS_scalar_b8_noslp := -DRTX_SRC=1 -DRTX_BATCH=8 -fno-slp-vectorize
+VARIANTS := g_lds_b4 p_lds_b4 g_lds_b4_pre g_lds_b4_max g_lds_b4_pre_max g_scalar_b8 g_scalar_b8_pre_max g_lds_b4_diagnobr
+VFLAGS_g_lds_b4           := -DRTX_SRC=0 -DRTX_BATCH=4
+VFLAGS_p_lds_b4           := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PERSISTENT=1
+VFLAGS_g_lds_b4_pre       := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PRETEST=1
+VFLAGS_g_lds_b4_max       := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_ANYMAX=1
+VFLAGS_g_lds_b4_pre_max   := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PRETEST=1 -DRTX_ANYMAX=1
+VFLAGS_g_scalar_b8        := -DRTX_SRC=1 -DRTX_BATCH=8
+VFLAGS_g_scalar_b8_pre_max := -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_PRETEST=1 -DRTX_ANYMAX=1
+VFLAGS_g_lds_b4_diagnobr  := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_DIAG_NOBRANCH=1
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

@@ -281,6 +281,7 @@ int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t npar
     p.scene = scene_of(c);
     p.out = out;
     p.counters = c->d_counters;
+    p.queue = reinterpret_cast<uint32_t *>(c->d_counters + 2);
     p.depth = c->depth;
     p.spp = c->spp;
     p.width = f.width;

@@ -32,6 +32,7 @@ struct KParams {
     KScene scene;
     float4 *out;                   // part's rows, contiguous, row-major
     unsigned long long *counters;  // [0] += ray segments (hit_world calls)
+    uint32_t *queue;               // pixel queue head (zeroed before each launch)
     uint32_t depth, spp;
     uint32_t width, rows_local;    // launch covers rows_local * width lanes
     uint32_t tile_rows, part, nparts;

@@ -68,6 +68,18 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 #define RTX_BATCH 4
 #endif
 static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
+#ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a queue; 0: one pixel per lane
+#define RTX_PERSISTENT 0
+#endif
+#ifndef RTX_PRETEST  // 1: skip roots of spheres entirely behind the ray (exact, see below)
+#define RTX_PRETEST 0
+#endif
+#ifndef RTX_ANYMAX  // 1: all-miss test on max(disc) instead of one ballot per sphere
+#define RTX_ANYMAX 0
+#endif
+#ifndef RTX_DIAG_NOBRANCH  // timing-only diagnostic: never compute roots (WRONG images)
+#define RTX_DIAG_NOBRANCH 0
+#endif
 
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
 // the near one is outside [t_min, best] (Sphere.cpp:15-24); strict
@@ -114,7 +126,7 @@ __device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0,
                 cz[q] = blk[16 + h + q];
                 nr2[q] = blk[24 + h + q];
             }
-            float hb[RTX_BATCH], disc[RTX_BATCH];
+            float hb[RTX_BATCH], disc[RTX_BATCH], cc[RTX_BATCH];
             uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < RTX_BATCH; ++k) {
@@ -122,16 +134,44 @@ __device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0,
                 const float ocy = o.y - cy[k];
                 const float ocz = o.z - cz[k];
                 hb[k] = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-                const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, nr2[k])));
-                disc[k] = fmaf(hb[k], hb[k], -(a * cc));
+                cc[k] = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, nr2[k])));
+                disc[k] = fmaf(hb[k], hb[k], -(a * cc[k]));
+#if !RTX_ANYMAX
                 any |= __ballot(!(disc[k] < 0.0f));
+#endif
             }
+#if RTX_ANYMAX
+            // max() drops a NaN operand: a batch mixing NaN and negative discs
+            // needs an fp32 overflow in hb^2 or a*cc (|coordinates| > ~1e18).
+            float m = disc[0];
+#pragma unroll
+            for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
+            any = __ballot(!(m < 0.0f));
+#endif
+#if RTX_DIAG_NOBRANCH
+#pragma unroll
+            for (int k = 0; k < RTX_BATCH; ++k) asm volatile("" ::"v"(disc[k]), "v"(hb[k]));
+            (void)any;
+#else
             if (any != 0ull) {
                 const int g = (int)(8 * (blk0 + b) + h);
 #pragma unroll
-                for (int k = 0; k < RTX_BATCH; ++k)
-                    if (!(disc[k] < 0.0f)) sphere_roots(hb[k], disc[k], inv_a, t_min, best, idx, g + k);
+                for (int k = 0; k < RTX_BATCH; ++k) {
+#if RTX_PRETEST
+                    // Sphere ahead of the origin? If hb > 0 and cc > 0 (origin
+                    // outside, moving away) both fp32 roots are < 0 <= t_min:
+                    // -hb - s < 0, and s = RN(sqrt(RN(hb^2 - x))) <= hb for
+                    // x = RN(a*cc) >= 0 because sqrt(RN(hb^2)) == hb when hb^2
+                    // is a normal number (1e-15 < hb < 1e18).
+                    const bool behind = hb[k] > 1e-15f && hb[k] < 1e18f && cc[k] > 0.0f;
+                    if (!(disc[k] < 0.0f) && !behind)
+#else
+                    if (!(disc[k] < 0.0f))
+#endif
+                        sphere_roots(hb[k], disc[k], inv_a, t_min, best, idx, g + k);
+                }
             }
+#endif
         }
     }
     return idx;
@@ -139,12 +179,13 @@ __device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0,
 
 typedef const __attribute__((address_space(4))) float *cfloat_p;  // constant AS: scalar loads
 
-// Lane state of one pixel's path tracer.
+// Lane state: the pixel it is tracing and that pixel's current path.
 struct Lane {
     f3 o, d, col, acc;
     float a, inv_a, seed;
     uint32_t sample, bounce, segs;
-    bool active;
+    uint32_t x, y, gid;  // pixel (global image coords) and its output slot
+    bool active;         // tracing a pixel
 };
 
 __device__ __forceinline__ void set_dir(Lane &L, f3 d) {
@@ -177,8 +218,18 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 // Shading of one finished hit_world call (sample_color body, :262-284, and
 // scatter, :207-252). Advances the lane to its next sample when the path
 // ends; clears `active` after the pixel's last sample.
-__device__ __forceinline__ void shade(const KParams &P, const Frame &F, uint32_t x, uint32_t y,
-                                      Lane &L, int hit, float t) {
+__device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
+    // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
+    const float spp = (float)P.spp;
+    float4 o;
+    o.x = to_gamma(L.acc.x / spp);
+    o.y = to_gamma(L.acc.y / spp);
+    o.z = to_gamma(L.acc.z / spp);
+    o.w = 1.0f;
+    P.out[L.gid] = o;
+}
+
+__device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
     L.segs++;
     bool ended = false;
     if (hit >= 0) {
@@ -234,10 +285,12 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, uint32_t
     }
     if (ended) {
         L.sample++;
-        if (L.sample >= P.spp)
+        if (L.sample >= P.spp) {
+            write_pixel(P, L);
             L.active = false;
-        else
-            begin_sample(P, F, x, y, L);
+        } else {
+            begin_sample(P, F, L.x, L.y, L);
+        }
     }
 }
 
@@ -249,23 +302,11 @@ __device__ __forceinline__ void lane_pixel(const KParams &P, uint32_t gid, uint3
     y = (j * P.nparts + P.part) * P.tile_rows + w;
 }
 
-__device__ __forceinline__ void finish(const KParams &P, uint32_t gid, const Lane &L, bool valid) {
-    // Segment counter: wave sum, one 64-bit atomic per wave.
-    uint32_t segs = valid ? L.segs : 0u;
+// Segment counter: wave sum, one 64-bit atomic per wave.
+__device__ __forceinline__ void count_segments(const KParams &P, uint32_t segs) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
-    if ((threadIdx.x & 63u) == 0u && segs != 0u)
-        atomicAdd(P.counters, (unsigned long long)segs);
-    if (valid) {
-        // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
-        const float spp = (float)P.spp;
-        float4 o;
-        o.x = to_gamma(L.acc.x / spp);
-        o.y = to_gamma(L.acc.y / spp);
-        o.z = to_gamma(L.acc.z / spp);
-        o.w = 1.0f;
-        P.out[gid] = o;
-    }
+    if ((threadIdx.x & 63u) == 0u && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
 }
 
 __device__ __forceinline__ Frame load_frame(const KParams &P) {
@@ -279,69 +320,101 @@ __device__ __forceinline__ Frame load_frame(const KParams &P) {
     return F;
 }
 
-__device__ __forceinline__ void init_lane(const KParams &P, const Frame &F, uint32_t x, uint32_t y,
-                                          bool valid, Lane &L) {
+// Start pixel `gid` (local index of this launch's rows) on this lane.
+// Launches with spp == 0 or depth == 0 never get here (k_render_trivial).
+__device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, uint32_t gid, Lane &L) {
+    L.gid = gid;
+    lane_pixel(P, gid, L.x, L.y);
     L.acc = mk3(0.0f, 0.0f, 0.0f);
-    L.col = mk3(1.0f, 1.0f, 1.0f);
-    L.o = mk3(0.0f, 0.0f, 0.0f);
-    L.d = mk3(0.0f, 0.0f, 1.0f);
-    L.a = 1.0f;
-    L.inv_a = 1.0f;
     L.sample = 0;
-    L.bounce = 0;
-    L.segs = 0;
-    L.seed = valid ? pixel_seed(P, x, y, 0) : 0.0f;
-    // depth 0: every sample returns black without tracing (:260, :286).
-    L.active = valid && P.spp > 0u && P.depth > 0u;
-    if (L.active) begin_sample(P, F, x, y, L);
+    L.seed = pixel_seed(P, L.x, L.y, 0);
+    L.active = true;
+    begin_sample(P, F, L.x, L.y, L);
 }
 
-// Sphere blocks resident in LDS (n_pad <= kResidentMax): waves run independently.
-__global__ void __launch_bounds__(kBlock) k_render_resident(const KParams P) {
-    extern __shared__ float4 s_blk4[];
-    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
+// Persistent-lane pixel queue: every idle lane of the wave takes the next
+// pixel index; ONE atomic per wave per refill (ballot + lane rank).
+// Returns true once the queue is exhausted (wave-uniform).
+__device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_t npix, Lane &L) {
+    const uint64_t idle = __ballot(!L.active);
+    if (idle == 0ull) return false;
+    const uint32_t cnt = (uint32_t)__popcll(idle);
+    const int leader = __ffsll((long long)idle) - 1;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(P.queue, cnt);
+    base = __shfl(base, leader, 64);
+    if (!L.active) {
+        const uint32_t g = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+        if (g < npix) start_pixel(P, F, g, L);
+    }
+    return base + cnt >= npix;
+}
+
+// Render kernel, per-wave independent: RTX_SRC 0 keeps the sphere blocks
+// resident in LDS (one copy per workgroup), 1 reads them with scalar loads.
+// RTX_PERSISTENT 1: the grid holds as many waves as the GPU keeps resident
+// and lanes pull pixels from the queue until it is exhausted; 0: exact grid,
+// one pixel per lane.
+__global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
     const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
+#if RTX_SRC == 0
+    extern __shared__ float4 s_blk4[];
+    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kBlock) s_blk4[i] = g4[i];
     __syncthreads();
-
-    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = gid < P.rows_local * P.width;
-    uint32_t x = 0, y = 0;
-    if (valid) lane_pixel(P, gid, x, y);
+#else
+    const cfloat_p soa = (cfloat_p)P.scene.soa;
+#endif
     const Frame F = load_frame(P);
+    const uint32_t npix = P.rows_local * P.width;
     Lane L;
-    init_lane(P, F, x, y, valid, L);
-
+    L.active = false;
+    L.segs = 0;
+#if RTX_PERSISTENT
+    bool exhausted = false;
+    for (;;) {
+        if (!exhausted) exhausted = refill(P, F, npix, L);
+        if (__ballot(L.active) == 0ull) break;  // spp, depth > 0: idle after refill => drained
+#else
+    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+    if (gid < npix) start_pixel(P, F, gid, L);
     while (__ballot(L.active) != 0ull) {
+#endif
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
+#if RTX_SRC == 0
             const int hit = hit_blocks(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
-            shade(P, F, x, y, L, min(hit, last), best);
+#else
+            const int hit = hit_blocks(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+#endif
+            shade(P, F, L, min(hit, last), best);
         }
     }
-    finish(P, gid, L, valid);
+    count_segments(P, L.segs);
 }
 
-// Large scenes (LDS variant): every ray segment streams the sphere blocks
-// through LDS in kChunk-sphere tiles shared by the block's 4 waves.
+// Large scenes with RTX_SRC 0: every ray segment streams the sphere blocks
+// through LDS in kChunk-sphere tiles shared by the block's 4 waves
+// (block-synchronous; the pixel queue is still per wave).
 __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
     extern __shared__ float4 s_blk4[];
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
-    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = gid < P.rows_local * P.width;
-    uint32_t x = 0, y = 0;
-    if (valid) lane_pixel(P, gid, x, y);
     const Frame F = load_frame(P);
+    const uint32_t npix = P.rows_local * P.width;
     Lane L;
-    init_lane(P, F, x, y, valid, L);
-
+    L.active = false;
+    L.segs = 0;
+    bool exhausted = false;
     constexpr uint32_t kChunkBlk = kChunk / 8;
-    while (__syncthreads_or(L.active ? 1 : 0)) {
+    for (;;) {
+        if (!exhausted) exhausted = refill(P, F, npix, L);
+        if (!__syncthreads_or(L.active ? 1 : 0)) break;
         float best = __uint_as_float(0x7f800000u);
         int hit = -1;
         for (uint32_t b0 = 0; b0 < nblk; b0 += kChunkBlk) {
@@ -351,34 +424,20 @@ __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
             __syncthreads();
             if (L.active) hit = hit_blocks(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit);
         }
-        if (L.active) shade(P, F, x, y, L, min(hit, last), best);
+        if (L.active) shade(P, F, L, min(hit, last), best);
     }
-    finish(P, gid, L, valid);
+    count_segments(P, L.segs);
 }
 
-// Scalar variant: sphere blocks read by wave-uniform scalar loads straight
-// from global memory (constant address space -> s_load into SGPRs); no LDS,
-// no block synchronisation, any n.
-__global__ void __launch_bounds__(kBlock) k_render_scalar(const KParams P) {
-    const uint32_t nblk = P.scene.n_pad / 8;
-    const int last = (int)P.scene.n - 1;
-    const cfloat_p soa = (cfloat_p)P.scene.soa;
+// spp == 0 or depth == 0: no segment is traced; the pixel is
+// toGamma(0 / spp) (accColor stays 0; 0/0 = NaN for spp == 0, :312-313).
+__global__ void __launch_bounds__(kBlock) k_render_trivial(const KParams P) {
     const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = gid < P.rows_local * P.width;
-    uint32_t x = 0, y = 0;
-    if (valid) lane_pixel(P, gid, x, y);
-    const Frame F = load_frame(P);
+    if (gid >= P.rows_local * P.width) return;
     Lane L;
-    init_lane(P, F, x, y, valid, L);
-
-    while (__ballot(L.active) != 0ull) {
-        if (L.active) {
-            float best = __uint_as_float(0x7f800000u);
-            const int hit = hit_blocks(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
-            shade(P, F, x, y, L, min(hit, last), best);
-        }
-    }
-    finish(P, gid, L, valid);
+    L.acc = mk3(0.0f, 0.0f, 0.0f);
+    L.gid = gid;
+    write_pixel(P, L);
 }
 
 // Gathered [nparts][max_rows][width] -> image [height][width].
@@ -456,18 +515,40 @@ inline uint32_t ceil_div(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1)
 
 }  // namespace
 
+// Workgroups the device keeps resident for `kern` (per-CU occupancy x CUs),
+// queried once per kernel/LDS size. Over-estimating is harmless: extra
+// workgroups find the pixel queue drained and exit.
+static uint32_t resident_blocks(const void *kern, size_t lds) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)kBlock, lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    return (uint32_t)(cus * per_cu);
+}
+
 hipError_t launch_render(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
-    const uint32_t blocks = ceil_div(lanes, kBlock);
-    if (RTX_SRC == 1) {
-        hipLaunchKernelGGL(k_render_scalar, dim3(blocks), dim3(kBlock), 0, stream, p);
-    } else if (p.scene.n_pad <= kResidentMax) {
-        const size_t lds = (size_t)(p.scene.n_pad ? p.scene.n_pad : 1) * sizeof(float4);
-        hipLaunchKernelGGL(k_render_resident, dim3(blocks), dim3(kBlock), lds, stream, p);
+    const uint32_t need = ceil_div(lanes, kBlock);
+    if (p.spp == 0 || p.depth == 0) {
+        hipLaunchKernelGGL(k_render_trivial, dim3(need), dim3(kBlock), 0, stream, p);
+        return hipGetLastError();
+    }
+    // Pixel queue head, zeroed on the stream ahead of the launch.
+    hipError_t e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
+        const size_t lds = RTX_SRC == 1 ? 0 : (size_t)(p.scene.n_pad ? p.scene.n_pad : 1) * sizeof(float4);
+        const uint32_t blocks =
+            RTX_PERSISTENT ? min(need, resident_blocks((const void *)k_render_persistent, lds)) : need;
+        hipLaunchKernelGGL(k_render_persistent, dim3(blocks), dim3(kBlock), lds, stream, p);
     } else {
-        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kBlock), kChunk * sizeof(float4),
-                           stream, p);
+        const size_t lds = kChunk * sizeof(float4);
+        const uint32_t blocks = min(need, resident_blocks((const void *)k_render_streamed, lds));
+        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kBlock), lds, stream, p);
     }
     return hipGetLastError();
 }
