@@ -45,15 +45,15 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := g_lds_b4 p_lds_b4 g_lds_b4_pre g_lds_b4_max g_lds_b4_pre_max g_scalar_b8 g_scalar_b8_pre_max g_lds_b4_diagnobr
-VFLAGS_g_lds_b4           := -DRTX_SRC=0 -DRTX_BATCH=4
-VFLAGS_p_lds_b4           := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PERSISTENT=1
-VFLAGS_g_lds_b4_pre       := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PRETEST=1
-VFLAGS_g_lds_b4_max       := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_ANYMAX=1
-VFLAGS_g_lds_b4_pre_max   := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_PRETEST=1 -DRTX_ANYMAX=1
-VFLAGS_g_scalar_b8        := -DRTX_SRC=1 -DRTX_BATCH=8
-VFLAGS_g_scalar_b8_pre_max := -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_PRETEST=1 -DRTX_ANYMAX=1
-VFLAGS_g_lds_b4_diagnobr  := -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_DIAG_NOBRANCH=1
+VARIANTS := seq_lds_b4 seq_scalar_b8 def_lds_b4 def_lds_b8 def_scalar_b4 def_scalar_b8 def_lds_b4_max def_scalar_b8_max
+VFLAGS_seq_lds_b4      := -DRTX_DEFER=0 -DRTX_SRC=0 -DRTX_BATCH=4
+VFLAGS_seq_scalar_b8   := -DRTX_DEFER=0 -DRTX_SRC=1 -DRTX_BATCH=8
+VFLAGS_def_lds_b4      := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4
+VFLAGS_def_lds_b8      := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8
+VFLAGS_def_scalar_b4   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=4
+VFLAGS_def_scalar_b8   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8
+VFLAGS_def_lds_b4_max  := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_ANYMAX=1
+VFLAGS_def_scalar_b8_max := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_ANYMAX=1
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

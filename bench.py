@@ -170,22 +170,21 @@ def main():
     ctx = rtx.Context(local_rank, stream=stream.cuda_stream)
     ctx.upload_world(world)
     ctx.set_frame(frame)
-    max_rows = rtx.part_rows(H, T, 0, R)
     dev = torch.device("cuda", local_rank)
-    image = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-    if R > 1:
-        send = torch.empty((max_rows, W, 4), dtype=torch.float32, device=dev)
-        gathered = torch.empty((R, max_rows, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
-        gather_list = list(gathered.unbind(0)) if rank == 0 else None
+    if R == 1:
+        image = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
 
-    def step():
-        if R == 1:
+        def step():
             ctx.render_rows(1, 0, 1, image.data_ptr())
-            return
-        ctx.render_rows(T, rank, R, send.data_ptr())
-        dist.gather(send, gather_list=gather_list, dst=0)
-        if rank == 0:
-            ctx.deinterleave(gathered.data_ptr(), W, H, T, R, image.data_ptr())
+    else:
+        from rtx.dist import FrameGather
+        fg = FrameGather(W, H, T, rank, R, device=dev,
+                         render_part=lambda send, part, nparts: ctx.render_rows(T, part, nparts, send.data_ptr()),
+                         deinterleave=lambda g, img: ctx.deinterleave(g.data_ptr(), W, H, T, R, img.data_ptr()))
+        image = fg.image
+
+        def step():
+            fg.step()
 
     def barrier():
         if R > 1:

@@ -87,6 +87,15 @@ typedef struct rtx_frame {
     uint32_t rng_mode;        /* RTX_RNG_*; 0 = reference                     */
     uint32_t frame_index;     /* seed offset for progressive frames; 0 = reference (time unused, :296) */
     uint32_t reserved[2];     /* must be 0 */
+    /* Thin-lens defocus (an extension: the reference's compute
+     * shader passes aperture but ignores it, DxCSApp.cpp:179 /
+     * ShaderCompute.hlsl:118-127). lens_u/lens_v = camera u/v axes, lens_u[3]
+     * = lens radius (aperture/2); 0 = pinhole (reference behaviour). Per
+     * sample: rd = radius * random_in_unit_disk (ShaderCompute.hlsl:50-57),
+     * offset = u*rd.x + v*rd.y, origin += offset, dir -= offset
+     * (Shader_RT.fx:288-298). */
+    float lens_u[4];
+    float lens_v[4];
 } rtx_frame;
 
 /* Counters of the last launches since rtx_stats_reset (measurement, §8d). */
@@ -137,6 +146,16 @@ RTX_API int rtx_render_rows(rtx_ctx *ctx, uint32_t tile_rows, uint32_t part,
                             uint32_t nparts, void *d_out);
 /* Whole frame into the context framebuffer (= rtx_render_rows(ctx,1,0,1,NULL)). */
 RTX_API int rtx_render(rtx_ctx *ctx);
+/* Progressive accumulation (the reference's intended
+ * interactive mode: sampleCount/currSamples DxCSApp.cpp:491-492, frame loop
+ * CSVersion/main.cpp:51-52, seed hook ShaderCompute.hlsl:296). reset != 0
+ * clears the accumulator. Each call renders one frame of spp samples per
+ * pixel with frame_index = frames accumulated so far (distinct seeds), adds
+ * each pixel's linear sample sum into a float4 accumulator, and writes
+ * toGamma(sum / (frames * spp)) into the context framebuffer. */
+RTX_API int rtx_accumulate(rtx_ctx *ctx, int reset);
+/* Frames accumulated since the last reset. */
+RTX_API uint32_t rtx_accumulated_frames(rtx_ctx *ctx);
 /* Rows owned by `part` (host arithmetic, no GPU). */
 RTX_API uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part,
                                uint32_t nparts);
@@ -191,6 +210,9 @@ RTX_API int rtx_camera_look_at(const float from[3], const float at[3],
                                float aperture, float focus_dist,
                                uint32_t width_px, uint32_t height_px,
                                rtx_frame *out);
+/* Enable thin-lens defocus on a frame from rtx_camera_look_at: lens
+ * radius = aperture / 2 (focus distance is already in the frame rows). */
+RTX_API int rtx_camera_set_aperture(rtx_frame *frame, float aperture);
 /* Camera(width, height) of the CPU library (Camera.h:9-21). */
 RTX_API int rtx_camera_simple(uint32_t width_px, uint32_t height_px, rtx_frame *out);
 /* Adapters from the reference's exact cbuffer byte layouts: WorldDef

@@ -31,7 +31,7 @@ class or_frame(C.Structure):
                 ("vertical", C.c_float * 4), ("lower_left", C.c_float * 4),
                 ("img_w", C.c_float), ("img_h", C.c_float), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("rng_mode", C.c_uint32), ("frame_index", C.c_uint32),
-                ("reserved", C.c_uint32 * 2)]
+                ("reserved", C.c_uint32 * 2), ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
 
 
 _lib = None
@@ -46,6 +46,8 @@ def lib() -> C.CDLL:
         f, d, u32 = C.POINTER(C.c_float), C.POINTER(C.c_double), C.c_uint32
         L.or_render_rows.argtypes = [C.POINTER(or_world), C.POINTER(or_frame), C.POINTER(u32), u32,
                                      f, C.c_int, C.c_int, C.POINTER(C.c_uint64)]
+        L.or_render_rows_linear.argtypes = [C.POINTER(or_world), C.POINTER(or_frame), C.POINTER(u32),
+                                            u32, f, C.c_int, C.POINTER(C.c_uint64)]
         L.or_hit_world_f32.argtypes = [C.POINTER(or_world), f, u32, C.c_float, C.c_float, f]
         L.or_hit_world_f64.argtypes = [d, u32, d, u32, C.c_double, C.c_double, d]
         L.or_camera_simple_rays_f64.argtypes = [u32, u32, d, u32, d]
@@ -97,6 +99,20 @@ def render_rows(world, frame, ys: Sequence[int], nthreads: int = 1, precision: i
                               ys.size, _f(out), nthreads, precision, C.byref(segs))
     if rc != 0:
         raise RuntimeError("or_render_rows failed")
+    del keep
+    return out, int(segs.value)
+
+
+def render_rows_linear(world, frame, ys: Sequence[int], nthreads: int = 1):
+    """Per-pixel linear sample sums (progressive-accumulation contribution)."""
+    ys = np.ascontiguousarray(ys, np.uint32)
+    f = frame_from(frame)
+    w, keep = _world_struct(world.spheres, world.mat_types, world.mat_values, world.depth, world.spp)
+    out = np.zeros((ys.size, f.width, 4), np.float32)
+    segs = C.c_uint64(0)
+    if lib().or_render_rows_linear(C.byref(w), C.byref(f), ys.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                   ys.size, _f(out), nthreads, C.byref(segs)) != 0:
+        raise RuntimeError("or_render_rows_linear failed")
     del keep
     return out, int(segs.value)
 

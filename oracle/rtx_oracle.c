@@ -171,6 +171,16 @@ static inline v3f rius(float *seed) {
     sincos_rt(phi, &sn, &cs);
     return v3(r * (sq * sn), r * (sq * cs), r * hx);
 }
+/* random_in_unit_disk, ShaderCompute.hlsl:50-57 (thin-lens extension) */
+static inline v3f rind(float *seed) {
+    float h0, h1;
+    hash2(seed, &h0, &h1);
+    const float phi = h1 * 6.28318530718f;
+    const float r = sqrtf(h0 * 1.0f);
+    float sn, cs;
+    sincos_rt(phi, &sn, &cs);
+    return v3(r * sn, r * cs, 0.0f);
+}
 static inline v3f reflect3(v3f v, v3f n) {
     const float k = 2.0f * vdot(v, n);
     return vsub(v, vscale(k, n));
@@ -346,6 +356,9 @@ typedef struct {
     v3f org, hor, ver, llc;
     float img_w, img_h;
     uint32_t width, rng_mode, frame_index;
+    v3f lu, lv;
+    float lens_r;
+    int linear; /* 1: write the linear sample sum instead of toGamma(sum/spp) */
 } frame32;
 
 static inline float pixel_seed(const frame32 *F, uint32_t spp, uint32_t x, uint32_t y, uint32_t s) {
@@ -372,6 +385,12 @@ static void pixel32(const scene32 *S, const frame32 *F, uint32_t x, uint32_t y, 
         const float v = ((float)y + g1 * 1.1f) / (F->img_h - 1.0f);
         v3f o = F->org;
         v3f d = vsub(vadd(vadd(F->llc, vscale(u, F->hor)), vscale(v, F->ver)), F->org);
+        if (F->lens_r > 0.0f) { /* thin lens, Shader_RT.fx:288-298 */
+            const v3f rd = vscale(F->lens_r, rind(&seed));
+            const v3f off = vadd(vscale(rd.x, F->lu), vscale(rd.y, F->lv));
+            o = vadd(o, off);
+            d = vsub(d, off);
+        }
         v3f col = v3(1.0f, 1.0f, 1.0f);
         /* sample_color, :255-287 */
         for (uint32_t k = 0; k < S->depth; ++k) {
@@ -421,9 +440,15 @@ static void pixel32(const scene32 *S, const frame32 *F, uint32_t x, uint32_t y, 
         }
     }
     const float spp = (float)S->spp;
-    out[0] = to_gamma(acc.x / spp);
-    out[1] = to_gamma(acc.y / spp);
-    out[2] = to_gamma(acc.z / spp);
+    if (F->linear) {
+        out[0] = acc.x;
+        out[1] = acc.y;
+        out[2] = acc.z;
+    } else {
+        out[0] = to_gamma(acc.x / spp);
+        out[1] = to_gamma(acc.y / spp);
+        out[2] = to_gamma(acc.z / spp);
+    }
     out[3] = 1.0f;
     *segs += sg;
 }
@@ -561,6 +586,15 @@ static void pixel64(const scene64 *S, const frame32 *F, uint32_t x, uint32_t y, 
         const double v = ((double)y + g1 * 1.1) / ((double)F->img_h - 1.0);
         v3d o = org;
         v3d d = dsub(dadd(dadd(llc, dscale(u, hor)), dscale(v, ver)), org);
+        if (F->lens_r > 0.0f) {
+            float h0d, h1d;
+            hash2(&seed, &h0d, &h1d);
+            const double rr = sqrt((double)h0d), ph = h1d * 6.28318530718;
+            const double rx = F->lens_r * rr * sin(ph), ry = F->lens_r * rr * cos(ph);
+            const v3d off = d3(rx * F->lu.x + ry * F->lv.x, rx * F->lu.y + ry * F->lv.y, rx * F->lu.z + ry * F->lv.z);
+            o = dadd(o, off);
+            d = dsub(d, off);
+        }
         v3d col = d3(1, 1, 1);
         for (uint32_t k = 0; k < S->depth; ++k) {
             double t;
@@ -654,8 +688,21 @@ static void *worker(void *arg) {
     return NULL;
 }
 
+static int render_rows_impl(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
+                            float *out, int nthreads, int precision, uint64_t *segments, int linear);
+
 int or_render_rows(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
                    float *out, int nthreads, int precision, uint64_t *segments) {
+    return render_rows_impl(w, f, ys, nys, out, nthreads, precision, segments, 0);
+}
+
+int or_render_rows_linear(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
+                          float *out, int nthreads, uint64_t *segments) {
+    return render_rows_impl(w, f, ys, nys, out, nthreads, 32, segments, 1);
+}
+
+static int render_rows_impl(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
+                            float *out, int nthreads, int precision, uint64_t *segments, int linear) {
     if (!w || !f || (nys && (!ys || !out)) || nthreads < 1) return -1;
     if (precision != 32 && precision != 64) return -1;
     frame32 F;
@@ -668,6 +715,10 @@ int or_render_rows(const or_world *w, const or_frame *f, const uint32_t *ys, uin
     F.width = f->width;
     F.rng_mode = f->rng_mode;
     F.frame_index = f->frame_index;
+    F.lu = v3(f->lens_u[0], f->lens_u[1], f->lens_u[2]);
+    F.lv = v3(f->lens_v[0], f->lens_v[1], f->lens_v[2]);
+    F.lens_r = f->lens_u[3];
+    F.linear = linear;
     scene32 S32;
     scene64 S64;
     memset(&S64, 0, sizeof(S64));
@@ -817,6 +868,8 @@ int or_camera_look_at(const float from[3], const float at[3], const float vup[3]
     out->horizontal[0] = H.x; out->horizontal[1] = H.y; out->horizontal[2] = H.z;
     out->vertical[0] = V.x; out->vertical[1] = V.y; out->vertical[2] = V.z;
     out->lower_left[0] = L.x; out->lower_left[1] = L.y; out->lower_left[2] = L.z; out->lower_left[3] = 1.0f;
+    out->lens_u[0] = u.x; out->lens_u[1] = u.y; out->lens_u[2] = u.z;
+    out->lens_v[0] = v.x; out->lens_v[1] = v.y; out->lens_v[2] = v.z;
     out->img_w = (float)width;
     out->img_h = (float)width / aspect;
     out->width = width;
@@ -835,6 +888,8 @@ int or_camera_simple(uint32_t width, uint32_t height, or_frame *out) {
     out->lower_left[1] = (float)(0.0 - vh / 2);
     out->lower_left[2] = -1.0f;
     out->lower_left[3] = 1.0f;
+    out->lens_u[0] = 1.0f;
+    out->lens_v[1] = 1.0f;
     out->img_w = (float)width;
     out->img_h = (float)height;
     out->width = width;

@@ -37,6 +37,7 @@ typedef struct or_frame {
     float origin[4], horizontal[4], vertical[4], lower_left[4];
     float img_w, img_h;
     uint32_t width, height, rng_mode, frame_index, reserved[2];
+    float lens_u[4], lens_v[4]; /* thin lens: axes, lens_u[3] = radius (0 = pinhole) */
 } or_frame;
 
 /* Render the listed global image rows (ys[0..nys)) into out
@@ -45,6 +46,11 @@ typedef struct or_frame {
  * *segments (optional) receives the number of hit_world calls. */
 int or_render_rows(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
                    float *out, int nthreads, int precision, uint64_t *segments);
+/* As or_render_rows (precision 32) but out receives each pixel's LINEAR
+ * sample sum (accColor before /spp and toGamma), w = 1: the per-frame
+ * contribution of progressive accumulation (rtx_accumulate). */
+int or_render_rows_linear(const or_world *w, const or_frame *f, const uint32_t *ys, uint32_t nys,
+                          float *out, int nthreads, uint64_t *segments);
 
 /* hit_world for a batch of rays (6 floats / 6 doubles each). out: 10 per
  * ray: hit, t, p.xyz, normal.xyz, front_face, index (same as

@@ -58,6 +58,9 @@ struct rtx_ctx {
     // framebuffer
     float4 *d_fb = nullptr;
     size_t fb_pixels = 0;
+    // progressive accumulation (linear sums), sized like the framebuffer
+    float4 *d_accum = nullptr;
+    uint32_t accum_frames = 0;
     // measurement
     unsigned long long *d_counters = nullptr;
     std::vector<EventPair> events;  // one pair per launch since reset
@@ -158,6 +161,7 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     free_world(c);
     (void)hipFree(c->d_fb);
+    (void)hipFree(c->d_accum);
     (void)hipFree(c->d_counters);
     for (auto &p : c->events) {
         (void)hipEventDestroy(p.start);
@@ -235,6 +239,7 @@ int rtx_set_frame(rtx_ctx *c, const rtx_frame *f) {
     if (f->width == 0 || f->height == 0)
         return fail(RTX_ERR_INVALID, "rtx_set_frame: zero width or height");
     if (f->rng_mode > 1) return fail(RTX_ERR_INVALID, "rtx_set_frame: unknown rng_mode");
+    if (!(f->lens_u[3] >= 0.0f)) return fail(RTX_ERR_INVALID, "rtx_set_frame: negative lens radius");
     if ((uint64_t)f->width * f->height > (1ull << 31))
         return fail(RTX_ERR_INVALID, "rtx_set_frame: more than 2^31 pixels");
     c->frame = *f;
@@ -253,8 +258,39 @@ uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part, uint3
     return rows;
 }
 
+static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
+                       float4 *accum, uint32_t accum_frames, uint32_t frame_index);
+
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
+    return render_impl(c, tile_rows, part, nparts, d_out, nullptr, 0, c->frame.frame_index);
+}
+
+int rtx_accumulate(rtx_ctx *c, int reset) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_accumulate: null ctx");
+    if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_accumulate: no frame set");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t px = (size_t)c->frame.width * c->frame.height;
+    if (reset || c->accum_frames == 0 || !c->d_accum || c->fb_pixels != px) {
+        if (!c->d_accum || c->fb_pixels != px) {
+            RTX_HIP(hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_accum);
+            c->d_accum = nullptr;
+            RTX_HIP(hipMalloc(&c->d_accum, px * sizeof(float4)));
+        }
+        RTX_HIP(hipMemsetAsync(c->d_accum, 0, px * sizeof(float4), c->stream));
+        c->accum_frames = 0;
+    }
+    rc = render_impl(c, 1, 0, 1, nullptr, c->d_accum, c->accum_frames + 1, c->accum_frames);
+    if (rc == RTX_OK) c->accum_frames++;
+    return rc;
+}
+
+uint32_t rtx_accumulated_frames(rtx_ctx *c) { return c ? c->accum_frames : 0; }
+
+static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
+                       float4 *accum, uint32_t accum_frames, uint32_t frame_index) {
     if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_render_rows: no world uploaded");
     if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_render_rows: no frame set");
     if (tile_rows == 0 || nparts == 0 || part >= nparts)
@@ -290,7 +326,14 @@ int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t npar
     p.part = part;
     p.nparts = nparts;
     p.rng_mode = f.rng_mode;
-    p.frame_index = f.frame_index;
+    p.frame_index = frame_index;
+    p.accum = accum;
+    p.accum_frames = accum_frames;
+    for (int k = 0; k < 3; ++k) {
+        p.lens_u[k] = f.lens_u[k];
+        p.lens_v[k] = f.lens_v[k];
+    }
+    p.lens_r = f.lens_u[3];
     for (int k = 0; k < 3; ++k) {
         p.org[k] = f.origin[k];
         p.hor[k] = f.horizontal[k];

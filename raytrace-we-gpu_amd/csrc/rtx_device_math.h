@@ -166,6 +166,18 @@ __device__ __forceinline__ f3 random_in_unit_sphere(float &seed) {
     sincos_rt(phi, sn, cs);
     return f3{r * (sq * sn), r * (sq * cs), r * hx};
 }
+// random_in_unit_disk (ShaderCompute.hlsl:50-57; unused by the reference,
+// used by the thin-lens extension): h = hash2 * (1, 2pi); r = sqrt(h.x);
+// r * (sin h.y, cos h.y). Returned as (x, y, 0).
+__device__ __forceinline__ f3 random_in_unit_disk(float &seed) {
+    float h0, h1;
+    hash2(seed, h0, h1);
+    const float phi = h1 * 6.28318530718f;
+    const float r = sqrtf(h0 * 1.0f);
+    float sn, cs;
+    sincos_rt(phi, sn, cs);
+    return f3{r * sn, r * cs, 0.0f};
+}
 // reflect(v, n) = v - 2*dot(v,n)*n   (:76-79)
 __device__ __forceinline__ f3 reflect3(f3 v, f3 n) {
     const float k = 2.0f * dot3(v, n);

@@ -150,6 +150,8 @@ int rtx_camera_look_at(const float from[3], const float at[3], const float vup[3
     set_row(out->horizontal, horizontal, 0.0f);
     set_row(out->vertical, vertical, 0.0f);
     set_row(out->lower_left, llc, 1.0f);
+    set_row(out->lens_u, u, 0.0f);  // lens radius 0: pinhole, as the reference shader
+    set_row(out->lens_v, v, 0.0f);
     out->img_w = (float)width_px;              // perspectiveVals.w
     out->img_h = (float)width_px / aspect;     // perspectiveVals.w / perspectiveVals.y
     out->width = width_px;
@@ -172,10 +174,18 @@ int rtx_camera_simple(uint32_t width_px, uint32_t height_px, rtx_frame *out) {
     out->lower_left[1] = (float)(0.0 - vh / 2);
     out->lower_left[2] = (float)(0.0 - 1.0);
     out->lower_left[3] = 1.0f;
+    out->lens_u[0] = 1.0f;  // Camera.h basis: u = +x, v = +y, pinhole
+    out->lens_v[1] = 1.0f;
     out->img_w = (float)width_px;
     out->img_h = (float)height_px;
     out->width = width_px;
     out->height = height_px;
+    return RTX_OK;
+}
+
+int rtx_camera_set_aperture(rtx_frame *frame, float aperture) {
+    if (!frame || !(aperture >= 0.0f)) return RTX_ERR_INVALID;
+    frame->lens_u[3] = aperture / 2.0f;  // f4w.w = aperture / 2 (DXRayTrace.cpp:52-57)
     return RTX_OK;
 }
 

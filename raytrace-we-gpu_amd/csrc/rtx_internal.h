@@ -39,11 +39,14 @@ struct KParams {
     uint32_t rng_mode, frame_index;
     float org[3], hor[3], ver[3], llc[3];
     float img_w, img_h;
+    float lens_u[3], lens_v[3], lens_r;  // thin lens (lens_r 0 = pinhole)
+    float4 *accum;                 // progressive accumulation (NULL = plain frame)
+    uint32_t accum_frames;         // frames in accum after this launch
 };
 
 // LDS variant: spheres kept resident in LDS up to this count (16 B each);
 // larger scenes are streamed through LDS in chunks of kChunk spheres.
-constexpr uint32_t kResidentMax = 4096;  // 64 KiB
+constexpr uint32_t kResidentMax = 4096;  // 64 KiB (+ 13 KiB candidate list)
 constexpr uint32_t kChunk = 1024;        // 16 KiB
 constexpr uint32_t kBlock = 256;         // 4 waves
 

@@ -38,6 +38,8 @@ constexpr float kTMin = 0.001f;  // hit_world(cur_ray, 0.001, 1.#INF, h), :262
 struct Frame {
     f3 org, hor, ver, llc;
     float img_w, img_h;
+    f3 lu, lv;
+    float lens_r;
 };
 
 // get_ray (ShaderCompute.hlsl:118-127): dir = llc + s*H + t*V - origin.
@@ -56,6 +58,12 @@ __device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_
     hash2(seed, g0, g1);
     const float v = ((float)y + g1 * 1.1f) / (F.img_h - 1.0f);
     get_ray(F, u, v, o, d);
+    if (F.lens_r > 0.0f) {  // thin lens (extension; pinhole ops above unchanged)
+        const f3 rd = F.lens_r * random_in_unit_disk(seed);
+        const f3 off = rd.x * F.lu + rd.y * F.lv;
+        o = o + off;
+        d = d - off;
+    }
 }
 
 // a = |d|^2 (Sphere.cpp:8; HLSL length(d)*length(d), :160), fma form.
@@ -80,6 +88,16 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_NOBRANCH  // timing-only diagnostic: never compute roots (WRONG images)
 #define RTX_DIAG_NOBRANCH 0
 #endif
+#ifndef RTX_DEFER  // 1: record candidates during the scan, resolve them afterwards
+#define RTX_DEFER 1
+#endif
+
+// Candidate list (RTX_DEFER): per lane kCand slots in LDS, slot-major
+// (slot j of lane t at [j * kBlock + t]: conflict-free), plus one dump slot
+// that absorbs writes past the end (the lane then falls back, see below).
+constexpr int kCand = 12;
+constexpr uint32_t kListBytes = (kCand + 1) * kBlock * sizeof(uint32_t);  // 13,312 B
+static_assert(kListBytes % 16 == 0, "LDS carve must stay 16-byte aligned");
 
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
 // the near one is outside [t_min, best] (Sphere.cpp:15-24); strict
@@ -111,9 +129,9 @@ __device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, 
 // reads issue together and one wave-uniform branch skips the root work
 // when no lane's ray line meets any of them (all-miss early out).
 template <typename Ptr>
-__device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d,
-                                          float a, float inv_a, float t_min, float &best,
-                                          int idx) {
+__device__ __forceinline__ int hit_blocks_seq(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d,
+                                              float a, float inv_a, float t_min, float &best,
+                                              int idx) {
     for (uint32_t b = 0; b < nblk; ++b) {
         const Ptr blk = soa + 32 * b;
 #pragma unroll
@@ -179,6 +197,120 @@ __device__ __forceinline__ int hit_blocks(Ptr soa, uint32_t nblk, uint32_t blk0,
 
 typedef const __attribute__((address_space(4))) float *cfloat_p;  // constant AS: scalar loads
 
+// ---- deferred candidate resolution ----------------------------------------
+// The sequential scan above accepts sphere i iff its candidate root
+//   c_i = rn if rn >= t_min, else rf if rf >= t_min, else none
+// satisfies c_i <= B_i, the running best (t_max initially) — rn > B_i makes
+// rf >= rn > B_i too, since s >= 0 and multiplying by inv_a > 0 is monotone
+// in fp32. c_i does not depend on B_i, so for finite roots the result is
+// (min c_i, largest index among the minima), in ANY evaluation order. The
+// scan therefore only records the spheres whose disc >= 0 (or NaN) in a
+// per-lane list and resolves them afterwards with all lanes working on
+// their own candidates at once, instead of running the sqrt/root code for
+// each sphere under the one or two lanes that need it. A lane with more
+// than kCand candidates, or any non-finite root (NaN/zero-length ray,
+// overflow), redoes the range with the exact sequential scan.
+template <typename Ptr>
+__device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o, f3 d, float a,
+                                                    uint32_t *list) {
+    uint32_t cnt = 0;
+    uint32_t *my = list + threadIdx.x;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const Ptr blk = soa + 32 * b;
+#pragma unroll
+        for (int h = 0; h < 8; h += RTX_BATCH) {
+            float disc[RTX_BATCH];
+            uint64_t any = 0;
+#pragma unroll
+            for (int k = 0; k < RTX_BATCH; ++k) {
+                const float ocx = o.x - blk[h + k];
+                const float ocy = o.y - blk[8 + h + k];
+                const float ocz = o.z - blk[16 + h + k];
+                const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+                const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + h + k])));
+                disc[k] = fmaf(hb, hb, -(a * cc));
+#if !RTX_ANYMAX
+                any |= __ballot(!(disc[k] < 0.0f));
+#endif
+            }
+#if RTX_ANYMAX
+            float m = disc[0];
+#pragma unroll
+            for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
+            any = __ballot(!(m < 0.0f));
+#endif
+            if (any != 0ull) {
+#pragma unroll
+                for (int k = 0; k < RTX_BATCH; ++k) {
+                    // write unconditionally at the next free slot (or the
+                    // dump slot), advance only for a candidate
+                    my[min(cnt, (uint32_t)kCand) * kBlock] = 8 * b + h + k;
+                    cnt += !(disc[k] < 0.0f) ? 1u : 0u;
+                }
+            }
+        }
+    }
+    return cnt;
+}
+
+// Resolve the lane's candidates (local indices into `soa`, global index =
+// 8*blk0 + local). Returns false if the lane must fall back.
+template <typename Ptr>
+__device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const uint32_t *list,
+                                                   uint32_t cnt, f3 o, f3 d, float a, float inv_a,
+                                                   float t_min, float &best, int &idx) {
+    bool ok = cnt <= (uint32_t)kCand;
+    const uint32_t m = ok ? cnt : 0u;
+    const float inf = __uint_as_float(0x7f800000u);
+    for (uint32_t j = 0; __ballot(j < m) != 0ull; ++j) {
+        if (j < m) {
+            const uint32_t i = list[j * kBlock + threadIdx.x];
+            const Ptr blk = soa + 32 * (i >> 3);
+            const uint32_t q = i & 7u;
+            const float ocx = o.x - blk[q];
+            const float ocy = o.y - blk[8 + q];
+            const float ocz = o.z - blk[16 + q];
+            const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+            const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + q])));
+            const float disc = fmaf(hb, hb, -(a * cc));
+            const float sq = sqrtf(disc);
+            const float rn = (-hb - sq) * inv_a;
+            const float rf = (-hb + sq) * inv_a;
+            if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) ok = false;
+            const bool use_n = !(rn < t_min);
+            const float c = use_n ? rn : rf;
+            const int g = (int)(8 * blk0 + i);
+            if ((use_n || !(rf < t_min)) && (c < best || (c == best && g > idx))) {
+                best = c;
+                idx = g;
+            }
+        }
+    }
+    return ok;
+}
+
+// hit_world over nblk sphere blocks (global block offset blk0), updating
+// (best, idx) exactly as the reference's in-order scan would.
+template <typename Ptr>
+__device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d, float a,
+                                         float inv_a, float t_min, float &best, int idx,
+                                         uint32_t *list) {
+#if RTX_DEFER && !RTX_DIAG_NOBRANCH
+    const float best0 = best;
+    const int idx0 = idx;
+    const uint32_t cnt = scan_candidates(soa, nblk, o, d, a, list);
+    if (!resolve_candidates(soa, blk0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
+        best = best0;
+        idx = hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx0);
+    }
+    return idx;
+#else
+    (void)list;
+    return hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx);
+#endif
+}
+
+
 // Lane state: the pixel it is tracing and that pixel's current path.
 struct Lane {
     f3 o, d, col, acc;
@@ -220,11 +352,21 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 // ends; clears `active` after the pixel's last sample.
 __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
     // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
-    const float spp = (float)P.spp;
+    f3 sum = L.acc;
+    float n = (float)P.spp;
+    if (P.accum) {  // progressive: running linear sum over frames
+        float4 a = P.accum[L.gid];
+        a.x = a.x + sum.x;
+        a.y = a.y + sum.y;
+        a.z = a.z + sum.z;
+        P.accum[L.gid] = a;
+        sum = mk3(a.x, a.y, a.z);
+        n = (float)(P.accum_frames * P.spp);
+    }
     float4 o;
-    o.x = to_gamma(L.acc.x / spp);
-    o.y = to_gamma(L.acc.y / spp);
-    o.z = to_gamma(L.acc.z / spp);
+    o.x = to_gamma(sum.x / n);
+    o.y = to_gamma(sum.y / n);
+    o.z = to_gamma(sum.z / n);
     o.w = 1.0f;
     P.out[L.gid] = o;
 }
@@ -317,6 +459,9 @@ __device__ __forceinline__ Frame load_frame(const KParams &P) {
     F.llc = mk3(P.llc[0], P.llc[1], P.llc[2]);
     F.img_w = P.img_w;
     F.img_h = P.img_h;
+    F.lu = mk3(P.lens_u[0], P.lens_u[1], P.lens_u[2]);
+    F.lv = mk3(P.lens_v[0], P.lens_v[1], P.lens_v[2]);
+    F.lens_r = P.lens_r;
     return F;
 }
 
@@ -357,10 +502,13 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // and lanes pull pixels from the queue until it is exhausted; 0: exact grid,
 // one pixel per lane.
 __global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
+    // dynamic LDS: [candidate list, kListBytes][sphere blocks (RTX_SRC 0)]
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
+    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
     const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
 #if RTX_SRC == 0
-    extern __shared__ float4 s_blk4[];
+    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kBlock) s_blk4[i] = g4[i];
@@ -386,9 +534,9 @@ __global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
 #if RTX_SRC == 0
-            const int hit = hit_blocks(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+            const int hit = hit_world(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
 #else
-            const int hit = hit_blocks(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1);
+            const int hit = hit_world(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
 #endif
             shade(P, F, L, min(hit, last), best);
         }
@@ -400,7 +548,9 @@ __global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
 // through LDS in kChunk-sphere tiles shared by the block's 4 waves
 // (block-synchronous; the pixel queue is still per wave).
 __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
-    extern __shared__ float4 s_blk4[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
+    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
+    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
@@ -422,7 +572,7 @@ __global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < 8 * cnt; i += kBlock) s_blk4[i] = g4[8 * b0 + i];
             __syncthreads();
-            if (L.active) hit = hit_blocks(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit);
+            if (L.active) hit = hit_world(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit, list);
         }
         if (L.active) shade(P, F, L, min(hit, last), best);
     }
@@ -458,6 +608,7 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
 __global__ void __launch_bounds__(kBlock) k_debug_hit_world(const KScene S, const float *rays,
                                                             uint32_t nrays, float t_min,
                                                             float t_max, float *out) {
+    __shared__ uint32_t list[kListBytes / sizeof(uint32_t)];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= nrays) return;
     const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
@@ -465,8 +616,8 @@ __global__ void __launch_bounds__(kBlock) k_debug_hit_world(const KScene S, cons
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx =
-        min(hit_blocks((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1), (int)S.n - 1);
+    const int idx = min(hit_world((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1, list),
+                        (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
         for (int k = 0; k < 10; ++k) r[k] = 0.0f;
@@ -529,6 +680,12 @@ static uint32_t resident_blocks(const void *kern, size_t lds) {
     return (uint32_t)(cus * per_cu);
 }
 
+// Dynamic LDS above 64 KiB must be opted into per kernel.
+static hipError_t allow_lds(const void *kern, size_t lds) {
+    if (lds <= 65536) return hipSuccess;
+    return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
 hipError_t launch_render(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
@@ -541,12 +698,14 @@ hipError_t launch_render(const KParams &p, hipStream_t stream) {
     hipError_t e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
-        const size_t lds = RTX_SRC == 1 ? 0 : (size_t)(p.scene.n_pad ? p.scene.n_pad : 1) * sizeof(float4);
+        const size_t lds = kListBytes + (RTX_SRC == 1 ? 0 : (size_t)p.scene.n_pad * sizeof(float4));
+        e = allow_lds((const void *)k_render_persistent, lds);
+        if (e != hipSuccess) return e;
         const uint32_t blocks =
             RTX_PERSISTENT ? min(need, resident_blocks((const void *)k_render_persistent, lds)) : need;
         hipLaunchKernelGGL(k_render_persistent, dim3(blocks), dim3(kBlock), lds, stream, p);
     } else {
-        const size_t lds = kChunk * sizeof(float4);
+        const size_t lds = kListBytes + kChunk * sizeof(float4);
         const uint32_t blocks = min(need, resident_blocks((const void *)k_render_streamed, lds));
         hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kBlock), lds, stream, p);
     }

@@ -47,7 +47,7 @@ class rtx_frame(C.Structure):
                 ("vertical", C.c_float * 4), ("lower_left", C.c_float * 4),
                 ("img_w", C.c_float), ("img_h", C.c_float), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("rng_mode", C.c_uint32), ("frame_index", C.c_uint32),
-                ("reserved", C.c_uint32 * 2)]
+                ("reserved", C.c_uint32 * 2), ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
 
 
 class rtx_stats(C.Structure):
@@ -81,6 +81,9 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_set_frame": (C.c_int, [ctx, C.POINTER(rtx_frame)]),
         "rtx_render_rows": (C.c_int, [ctx, u32, u32, u32, vp]),
         "rtx_render": (C.c_int, [ctx]),
+        "rtx_accumulate": (C.c_int, [ctx, C.c_int]),
+        "rtx_accumulated_frames": (u32, [ctx]),
+        "rtx_camera_set_aperture": (C.c_int, [C.POINTER(rtx_frame), C.c_float]),
         "rtx_part_rows": (u32, [u32, u32, u32, u32]),
         "rtx_deinterleave_rows": (C.c_int, [ctx, vp, u32, u32, u32, u32, vp]),
         "rtx_sync": (C.c_int, [ctx]),
@@ -187,6 +190,12 @@ def camera_look_at(width: int, height: int, look_from=(13.0, 2.0, 3.0), look_at=
     return f
 
 
+def set_aperture(frame: rtx_frame, aperture: float) -> rtx_frame:
+    """Thin-lens defocus: lens radius = aperture / 2."""
+    _check(load_library().rtx_camera_set_aperture(C.byref(frame), aperture), "rtx_camera_set_aperture")
+    return frame
+
+
 def camera_simple(width: int, height: int) -> rtx_frame:
     """Camera(width, height) of the CPU library (Camera.h:9-21)."""
     f = rtx_frame()
@@ -263,6 +272,11 @@ class Context:
 
     def render(self):
         _check(self._lib.rtx_render(self._h), "rtx_render")
+
+    def accumulate(self, reset: bool = False) -> int:
+        """Progressive accumulation; returns frames accumulated."""
+        _check(self._lib.rtx_accumulate(self._h, 1 if reset else 0), "rtx_accumulate")
+        return int(self._lib.rtx_accumulated_frames(self._h))
 
     def deinterleave(self, d_gathered: int, width: int, height: int, tile_rows: int, nparts: int,
                      d_image: int):

@@ -245,3 +245,44 @@ def test_partitions_reassemble_bit_identical(gpu_ctx, rtx, nparts, tile_rows):
     assert_bits_equal(image.numpy(), full, f"{nparts} parts x {tile_rows}-row tiles")
     gathered.free()
     image.free()
+
+
+# ---------------------------------------------------------------------------
+# §8f rows: thin lens (f-3) and progressive accumulation (f-2)
+# ---------------------------------------------------------------------------
+def test_thin_lens_bit_exact(gpu_ctx, oracle, rtx):
+    """Defocus: lens offset from random_in_unit_disk (ShaderCompute.hlsl:50-57)
+    applied as in Shader_RT.fx:288-298; bit-exact vs the oracle."""
+    world = rtx.random_world(11, depth=50, spp=4)
+    frame = rtx.set_aperture(rtx.camera_look_at(160, 90, aspect=160 / 90), 0.4)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(90), nthreads=8)
+    assert_bits_equal(img, want, "thin lens")
+    assert st.segments == segs
+
+
+def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
+    """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
+    fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
+    W, H, spp = 64, 36, 2
+    world = rtx.random_world(11, depth=20, spp=spp)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(frame)
+    total = np.zeros((H, W, 4), np.float32)
+    for k in range(3):
+        assert gpu_ctx.accumulate(reset=(k == 0)) == k + 1
+        f = rtx.camera_look_at(W, H, aspect=W / H)
+        f.frame_index = k
+        lin, _ = oracle.render_rows_linear(world, f, np.arange(H), nthreads=8)
+        total[..., :3] = total[..., :3] + lin[..., :3]
+        mean = (total[..., :3] / np.float32((k + 1) * spp)).astype(np.float32)
+        want = np.ones((H, W, 4), np.float32)
+        want[..., :3] = oracle.math("pow", mean.ravel(), np.full(mean.size, 0.454545454545, np.float32)).reshape(mean.shape)
+        assert_bits_equal(gpu_ctx.download(), want, f"accumulated frame {k + 1}")
+    # frame 1 of the accumulation is the plain reference frame
+    assert gpu_ctx.accumulate(reset=True) == 1
+    plain, _ = render_gpu(gpu_ctx, world, frame)
+    gpu_ctx.set_frame(frame)
+    gpu_ctx.accumulate(reset=True)
+    assert_bits_equal(gpu_ctx.download(), plain, "1-frame accumulation == plain frame")

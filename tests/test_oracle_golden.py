@@ -105,3 +105,13 @@ def test_oracle_row_order_and_threads_invariant(oracle, rtx):
     b, sb = oracle.render_rows(world, frame, rows[::-1].copy(), nthreads=5)
     np.testing.assert_array_equal(a.view(np.uint32), b[::-1].view(np.uint32))
     assert sa == sb
+
+
+def test_thin_lens_changes_only_when_enabled(oracle, rtx):
+    world = rtx.random_world(4, depth=10, spp=2)
+    pin = rtx.camera_look_at(32, 18, aspect=32 / 18)
+    a, _ = oracle.render_rows(world, pin, np.arange(18))
+    b, _ = oracle.render_rows(world, rtx.set_aperture(rtx.camera_look_at(32, 18, aspect=32 / 18), 0.0), np.arange(18))
+    c, _ = oracle.render_rows(world, rtx.set_aperture(rtx.camera_look_at(32, 18, aspect=32 / 18), 0.5), np.arange(18))
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a != c).mean() > 0.1
