@@ -45,15 +45,10 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := seq_lds_b4 seq_scalar_b8 def_lds_b4 def_lds_b8 def_scalar_b4 def_scalar_b8 def_lds_b4_max def_scalar_b8_max
-VFLAGS_seq_lds_b4      := -DRTX_DEFER=0 -DRTX_SRC=0 -DRTX_BATCH=4
-VFLAGS_seq_scalar_b8   := -DRTX_DEFER=0 -DRTX_SRC=1 -DRTX_BATCH=8
-VFLAGS_def_lds_b4      := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4
-VFLAGS_def_lds_b8      := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8
-VFLAGS_def_scalar_b4   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=4
-VFLAGS_def_scalar_b8   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8
-VFLAGS_def_lds_b4_max  := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_ANYMAX=1
-VFLAGS_def_scalar_b8_max := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_ANYMAX=1
+VARIANTS := best lds_stream_b8 lds_stream_b4
+VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
+VFLAGS_lds_stream_b8 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
+VFLAGS_lds_stream_b4 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

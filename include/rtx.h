@@ -243,6 +243,11 @@ enum {
 };
 RTX_API int rtx_debug_math(rtx_ctx *ctx, int fn, const float *in0,
                            const float *in1, uint32_t n, float *out);
+/* Wave timeline diagnostic: a call with a new max_waves (> 0) arms
+ * recording of every render wave's (start, end) s_memrealtime (100 MHz)
+ * into a device buffer of that many waves (0 disarms); a call with the same
+ * max_waves and host_pairs != NULL copies the pairs back (synchronous). */
+RTX_API int rtx_debug_wave_times(rtx_ctx *ctx, size_t max_waves, unsigned long long *host_pairs);
 
 #ifdef __cplusplus
 }

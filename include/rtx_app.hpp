@@ -60,6 +60,7 @@ struct AppConfig {
     float aspect = 16.0f / 9.0f;
     float aperture = 2.0f;
     bool simple_camera = false;            // Camera.h instead of ComputeViewVals
+    float lens_aperture = 0.0f;            // > 0: thin lens (extension, §8f-3); 0 = reference pinhole
     uint32_t rng_mode = RTX_RNG_CHAIN;
 };
 

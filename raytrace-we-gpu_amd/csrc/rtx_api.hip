@@ -63,6 +63,8 @@ struct rtx_ctx {
     uint32_t accum_frames = 0;
     // measurement
     unsigned long long *d_counters = nullptr;
+    unsigned long long *d_wave_times = nullptr;  // diagnostic (rtx_debug_wave_times)
+    size_t wave_times_cap = 0;
     std::vector<EventPair> events;  // one pair per launch since reset
     size_t events_used = 0;
     uint64_t samples = 0;
@@ -163,6 +165,7 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipFree(c->d_fb);
     (void)hipFree(c->d_accum);
     (void)hipFree(c->d_counters);
+    (void)hipFree(c->d_wave_times);
     for (auto &p : c->events) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
@@ -182,6 +185,16 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (w->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_upload_world: reserved must be 0");
     if (w->count > 0 && (!w->spheres || !w->mat_types || !w->mat_values))
         return fail(RTX_ERR_INVALID, "rtx_upload_world: null array with count > 0");
+    // Exactness bound of the kernel's all-miss test (rtx_kernels.hip,
+    // RTX_ANYMAX): finite scene values of magnitude <= 1e15 keep every
+    // ray-sphere discriminant of a finite ray free of fp32 overflow.
+    for (uint32_t i = 0; i < w->count; ++i)
+        for (int k = 0; k < 4; ++k) {
+            const float v = w->spheres[4 * i + k];
+            if (!(v >= -1e15f && v <= 1e15f))
+                return fail(RTX_ERR_INVALID, "rtx_upload_world: sphere " + std::to_string(i) +
+                                                 " has a non-finite or |value| > 1e15 component");
+        }
     int rc = set_device(c);
     if (rc) return rc;
     const uint32_t n = w->count;
@@ -334,6 +347,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         p.lens_v[k] = f.lens_v[k];
     }
     p.lens_r = f.lens_u[3];
+    p.wave_times = c->d_wave_times;
     for (int k = 0; k < 3; ++k) {
         p.org[k] = f.origin[k];
         p.hor[k] = f.horizontal[k];
@@ -471,6 +485,30 @@ int rtx_copy_to_device(rtx_ctx *c, void *d_dst, const void *host, size_t bytes) 
     if (rc) return rc;
     RTX_HIP(hipMemcpyAsync(d_dst, host, bytes, hipMemcpyHostToDevice, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+int rtx_debug_wave_times(rtx_ctx *c, size_t max_waves, unsigned long long *host_pairs) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_debug_wave_times: null ctx");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (max_waves != c->wave_times_cap) {  // (re)arm: allocate and enable recording
+        RTX_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_wave_times);
+        c->d_wave_times = nullptr;
+        c->wave_times_cap = 0;
+        if (max_waves) {
+            RTX_HIP(hipMalloc(&c->d_wave_times, max_waves * 2 * sizeof(unsigned long long)));
+            RTX_HIP(hipMemsetAsync(c->d_wave_times, 0, max_waves * 2 * sizeof(unsigned long long), c->stream));
+            c->wave_times_cap = max_waves;
+        }
+        return RTX_OK;
+    }
+    if (host_pairs && max_waves) {
+        RTX_HIP(hipMemcpyAsync(host_pairs, c->d_wave_times, max_waves * 2 * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, c->stream));
+        RTX_HIP(hipStreamSynchronize(c->stream));
+    }
     return RTX_OK;
 }
 

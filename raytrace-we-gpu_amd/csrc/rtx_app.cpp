@@ -87,6 +87,7 @@ void RtxCSApp::Update() {
         rc = rtx_camera_look_at(m_cfg.cam_pos, m_cfg.cam_look_at, m_cfg.up, m_cfg.vfov, m_cfg.aspect,
                                 m_cfg.aperture, 0.0f, m_cfg.width, m_cfg.height, &m_frame);
     m_frame.rng_mode = m_cfg.rng_mode;
+    if (rc == RTX_OK && m_cfg.lens_aperture > 0.0f) rc = rtx_camera_set_aperture(&m_frame, m_cfg.lens_aperture);
     ++m_frame_count;
     if (rc != RTX_OK || rtx_set_frame(m_ctx, &m_frame) != RTX_OK) {
         m_error = rtx_last_error();

@@ -6,7 +6,10 @@
 //   rtx_cli [--width W] [--height H] [--spp S] [--depth D]
 //           [--scene rtiow9|rtiow11|test|random:EXT[:MAX]] [--simple-camera]
 //           [--rng chain|per-sample] [--frames K] [--device N]
+//           [--aperture A] [--accumulate]
 //           [--pfm out.pfm] [--ppm out.ppm]
+// --accumulate renders the K frames progressively (rtx_accumulate) instead
+// of K independent frames; --aperture enables the thin lens.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -21,7 +24,7 @@ static void usage() {
                  "usage: rtx_cli [--width W] [--height H] [--spp S] [--depth D]\n"
                  "               [--scene rtiow9|rtiow11|test|random:EXT[:MAX]] [--simple-camera]\n"
                  "               [--rng chain|per-sample] [--frames K] [--device N]\n"
-                 "               [--pfm FILE] [--ppm FILE]\n");
+                 "               [--aperture A] [--accumulate] [--pfm FILE] [--ppm FILE]\n");
 }
 
 int main(int argc, char **argv) {
@@ -32,6 +35,7 @@ int main(int argc, char **argv) {
     cfg.depth = 50;
     cfg.grid_half_extent = 11;
     int frames = 1, device = 0;
+    bool accumulate = false;
     std::string pfm, ppm;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -51,6 +55,8 @@ int main(int argc, char **argv) {
         else if (a == "--pfm") pfm = next();
         else if (a == "--ppm") ppm = next();
         else if (a == "--simple-camera") cfg.simple_camera = true;
+        else if (a == "--aperture") cfg.lens_aperture = (float)std::atof(next());
+        else if (a == "--accumulate") accumulate = true;
         else if (a == "--rng") {
             const std::string m = next();
             cfg.rng_mode = (m == "per-sample") ? RTX_RNG_PER_SAMPLE : RTX_RNG_CHAIN;
@@ -93,7 +99,14 @@ int main(int argc, char **argv) {
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = 0; k < frames; ++k) {
         app.Update();
-        app.Render();
+        if (accumulate) {
+            if (rtx_accumulate(app.context(), k == 0) != RTX_OK) {
+                std::fprintf(stderr, "rtx_cli: accumulate failed: %s\n", rtx_last_error());
+                return 1;
+            }
+        } else {
+            app.Render();
+        }
     }
     rtx_sync(app.context());
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

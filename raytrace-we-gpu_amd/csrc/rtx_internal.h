@@ -42,6 +42,7 @@ struct KParams {
     float lens_u[3], lens_v[3], lens_r;  // thin lens (lens_r 0 = pinhole)
     float4 *accum;                 // progressive accumulation (NULL = plain frame)
     uint32_t accum_frames;         // frames in accum after this launch
+    unsigned long long *wave_times;  // diagnostic: per-wave (start, end) s_memrealtime, or NULL
 };
 
 // LDS variant: spheres kept resident in LDS up to this count (16 B each);

@@ -70,10 +70,10 @@ __device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_
 __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y, d.y, d.x * d.x)); }
 
 #ifndef RTX_SRC
-#define RTX_SRC 0
+#define RTX_SRC 1
 #endif
 #ifndef RTX_BATCH
-#define RTX_BATCH 4
+#define RTX_BATCH 8
 #endif
 static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a queue; 0: one pixel per lane
@@ -83,13 +83,24 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #define RTX_PRETEST 0
 #endif
 #ifndef RTX_ANYMAX  // 1: all-miss test on max(disc) instead of one ballot per sphere
-#define RTX_ANYMAX 0
+#define RTX_ANYMAX 1
 #endif
 #ifndef RTX_DIAG_NOBRANCH  // timing-only diagnostic: never compute roots (WRONG images)
 #define RTX_DIAG_NOBRANCH 0
 #endif
 #ifndef RTX_DEFER  // 1: record candidates during the scan, resolve them afterwards
 #define RTX_DEFER 1
+#endif
+#ifndef RTX_LISTMASK  // 1: one list entry per 4-sphere batch (index | 4-bit mask << 28)
+#define RTX_LISTMASK 1
+#endif
+#ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
+#define RTX_WAVES_PER_SIMD 0
+#endif
+#if RTX_WAVES_PER_SIMD
+#define RTX_RENDER_BOUNDS __launch_bounds__(kBlock, RTX_WAVES_PER_SIMD)
+#else
+#define RTX_RENDER_BOUNDS __launch_bounds__(kBlock)
 #endif
 
 // Candidate list (RTX_DEFER): per lane kCand slots in LDS, slot-major
@@ -160,7 +171,9 @@ __device__ __forceinline__ int hit_blocks_seq(Ptr soa, uint32_t nblk, uint32_t b
             }
 #if RTX_ANYMAX
             // max() drops a NaN operand: a batch mixing NaN and negative discs
-            // needs an fp32 overflow in hb^2 or a*cc (|coordinates| > ~1e18).
+            // needs an fp32 overflow in hb^2 or a*cc, which rtx_upload_world's
+            // bound (|scene values| <= 1e15) rules out; an all-NaN batch (NaN
+            // ray) yields NaN and is taken, like the reference.
             float m = disc[0];
 #pragma unroll
             for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
@@ -240,6 +253,15 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
             any = __ballot(!(m < 0.0f));
 #endif
             if (any != 0ull) {
+#if RTX_LISTMASK
+#pragma unroll
+                for (int q = 0; q < RTX_BATCH; q += 4) {
+                    const uint32_t m = (!(disc[q] < 0.0f) ? 1u : 0u) | (!(disc[q + 1] < 0.0f) ? 2u : 0u) |
+                                       (!(disc[q + 2] < 0.0f) ? 4u : 0u) | (!(disc[q + 3] < 0.0f) ? 8u : 0u);
+                    my[min(cnt, (uint32_t)kCand) * kBlock] = (8 * b + h + q) | (m << 28);
+                    cnt += m != 0u ? 1u : 0u;
+                }
+#else
 #pragma unroll
                 for (int k = 0; k < RTX_BATCH; ++k) {
                     // write unconditionally at the next free slot (or the
@@ -247,6 +269,7 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
                     my[min(cnt, (uint32_t)kCand) * kBlock] = 8 * b + h + k;
                     cnt += !(disc[k] < 0.0f) ? 1u : 0u;
                 }
+#endif
             }
         }
     }
@@ -262,9 +285,22 @@ __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const
     bool ok = cnt <= (uint32_t)kCand;
     const uint32_t m = ok ? cnt : 0u;
     const float inf = __uint_as_float(0x7f800000u);
+#if RTX_LISTMASK
+    uint32_t j = 0, e = 0;  // entry index, remaining mask bits of entry j
+    if (m) e = list[threadIdx.x];
+    for (;;) {
+        const bool live = j < m;
+        if (__ballot(live) == 0ull) break;
+        if (live) {
+            const uint32_t bits = e >> 28;
+            const uint32_t i = (e & 0x0fffffffu) + (uint32_t)__builtin_ctz(bits);
+            e &= ~(1u << (28 + __builtin_ctz(bits)));
+            if ((e >> 28) == 0u && ++j < m) e = list[j * kBlock + threadIdx.x];
+#else
     for (uint32_t j = 0; __ballot(j < m) != 0ull; ++j) {
         if (j < m) {
             const uint32_t i = list[j * kBlock + threadIdx.x];
+#endif
             const Ptr blk = soa + 32 * (i >> 3);
             const uint32_t q = i & 7u;
             const float ocx = o.x - blk[q];
@@ -501,7 +537,7 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // RTX_PERSISTENT 1: the grid holds as many waves as the GPU keeps resident
 // and lanes pull pixels from the queue until it is exhausted; 0: exact grid,
 // one pixel per lane.
-__global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
+__global__ void RTX_RENDER_BOUNDS k_render_persistent(const KParams P) {
     // dynamic LDS: [candidate list, kListBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -518,6 +554,7 @@ __global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
 #endif
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
+    const unsigned long long t_start = P.wave_times ? __builtin_amdgcn_s_memrealtime() : 0ull;
     Lane L;
     L.active = false;
     L.segs = 0;
@@ -542,12 +579,17 @@ __global__ void __launch_bounds__(kBlock) k_render_persistent(const KParams P) {
         }
     }
     count_segments(P, L.segs);
+    if (P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
+        const uint32_t w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+        P.wave_times[2 * w] = t_start;
+        P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // Large scenes with RTX_SRC 0: every ray segment streams the sphere blocks
 // through LDS in kChunk-sphere tiles shared by the block's 4 waves
 // (block-synchronous; the pixel queue is still per wave).
-__global__ void __launch_bounds__(kBlock) k_render_streamed(const KParams P) {
+__global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
     float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);

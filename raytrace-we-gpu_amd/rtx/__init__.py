@@ -104,6 +104,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_frame_from_perframe": (C.c_int, [vp, C.c_size_t, u32, u32, C.POINTER(rtx_frame)]),
         "rtx_debug_hit_world": (C.c_int, [ctx, f, u32, C.c_float, C.c_float, f]),
         "rtx_debug_math": (C.c_int, [ctx, C.c_int, f, f, u32, f]),
+        "rtx_debug_wave_times": (C.c_int, [ctx, C.c_size_t, C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -317,6 +318,15 @@ class Context:
         out = np.zeros((rays.shape[0], 10), np.float32)
         _check(self._lib.rtx_debug_hit_world(self._h, _fptr(rays), rays.shape[0], t_min, t_max,
                                              _fptr(out)), "rtx_debug_hit_world")
+        return out
+
+    def arm_wave_times(self, max_waves: int):
+        _check(self._lib.rtx_debug_wave_times(self._h, max_waves, None), "rtx_debug_wave_times", self._lib)
+
+    def wave_times(self, max_waves: int) -> np.ndarray:
+        out = np.zeros((max_waves, 2), np.uint64)
+        _check(self._lib.rtx_debug_wave_times(self._h, max_waves, out.ctypes.data_as(C.POINTER(C.c_uint64))),
+               "rtx_debug_wave_times", self._lib)
         return out
 
     def debug_math(self, fn: str, in0: np.ndarray, in1: Optional[np.ndarray] = None) -> np.ndarray:

@@ -286,3 +286,39 @@ def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     gpu_ctx.set_frame(frame)
     gpu_ctx.accumulate(reset=True)
     assert_bits_equal(gpu_ctx.download(), plain, "1-frame accumulation == plain frame")
+
+
+def test_cli_writes_reference_frame(tmp_path, oracle, rtx):
+    """rtx_cli (the headless DxCSApp driver) renders the frame the oracle renders;
+    its PFM stores rows bottom-to-top like the framebuffer."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "raytrace-we-gpu_amd", "bin", "rtx_cli")
+    pfm = str(tmp_path / "f.pfm")
+    out = subprocess.run([cli, "--width", "64", "--height", "36", "--spp", "3", "--depth", "50",
+                          "--scene", "rtiow11", "--frames", "1", "--pfm", pfm],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    with open(pfm, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        assert float(f.readline()) < 0  # little endian
+        img = np.frombuffer(f.read(), "<f4").reshape(h, w, 3)
+    world = rtx.random_world(11, depth=50, spp=3)
+    frame = rtx.camera_look_at(64, 36, aspect=64 / 36)
+    want, _ = oracle.render_rows(world, frame, np.arange(36), nthreads=4)
+    assert_bits_equal(img, want[..., :3], "rtx_cli PFM")
+
+
+def test_upload_rejects_out_of_range_scene(gpu_ctx, rtx):
+    """Scene values must be finite with |v| <= 1e15 (the all-miss test's
+    exactness bound, rtx_api.hip); the context stays usable afterwards."""
+    w = rtx.random_world(2, depth=4, spp=1)
+    bad = rtx.World(w.spheres.copy(), w.mat_types, w.mat_values, 4, 1)
+    bad.spheres[3, 0] = np.inf
+    with pytest.raises(rtx.RtxError, match="1e15"):
+        gpu_ctx.upload_world(bad)
+    bad.spheres[3, 0] = 2e15
+    with pytest.raises(rtx.RtxError):
+        gpu_ctx.upload_world(bad)
+    gpu_ctx.upload_world(w)

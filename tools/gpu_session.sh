@@ -33,11 +33,20 @@ for s in $STEPS; do
                 python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
     variants) run variants 900 python tools/variant_bench.py --rounds 3 --frames 2 ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
+    timeline) run timeline 300 python tools/wave_timeline.py ;;
+    c5)     run c5 900 python tools/variant_bench.py --rounds 2 --frames 1 --spp 16 --grid 159 --max-spheres 100000 $C5V ;;
     diag)   run diag 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
                 SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/diag" -o run -- \
                 python3 bench.py --probe ;;
     diag2)  run diag2 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM \
                 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/diag2" -o run -- \
+                python3 bench.py --probe ;;
+    vdiag)  V=raytrace-we-gpu_amd/lib/variants/librtx_${VDIAG:-best}.so
+            RTX_LIB=$V run vdiag 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES \
+                SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/vdiag" -o run -- \
+                python3 bench.py --probe
+            RTX_LIB=$V run vdiag2 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
+                SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d "$OUT/vdiag2" -o run -- \
                 python3 bench.py --probe ;;
     pmc)    for c in FETCH_SIZE WRITE_SIZE; do
               run pmc_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
