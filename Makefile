@@ -45,10 +45,20 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best lds_stream_b8 lds_stream_b4
+VARIANTS := blk64 lpt lpt_s2 lpt_cw4 lpt_s2_cw4
 VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
+VFLAGS_blk64         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=64
+VFLAGS_blk128        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=128
+VFLAGS_blk64_w7      := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=64 -DRTX_WAVES_PER_SIMD=7
+VFLAGS_lpt           := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1
+VFLAGS_lpt_blk64     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_BLOCK=64
+VFLAGS_lpt_r0        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_RADIUS=0
+VFLAGS_lpt_r2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_RADIUS=2
+VFLAGS_lpt_s2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2
+VFLAGS_lpt_cw4       := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_CW=4
+VFLAGS_lpt_s2_cw4    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2 -DRTX_LPT_CW=4
+VFLAGS_lpt_blk128    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_BLOCK=128
 VFLAGS_lds_stream_b8 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
-VFLAGS_lds_stream_b4 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=4 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

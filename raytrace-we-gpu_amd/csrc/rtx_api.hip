@@ -65,6 +65,9 @@ struct rtx_ctx {
     unsigned long long *d_counters = nullptr;
     unsigned long long *d_wave_times = nullptr;  // diagnostic (rtx_debug_wave_times)
     size_t wave_times_cap = 0;
+    // LPT scheduling scratch (persistent kernel): cost + perm per pixel
+    uint32_t *d_sched = nullptr;
+    size_t sched_pixels = 0;
     std::vector<EventPair> events;  // one pair per launch since reset
     size_t events_used = 0;
     uint64_t samples = 0;
@@ -166,6 +169,7 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipFree(c->d_accum);
     (void)hipFree(c->d_counters);
     (void)hipFree(c->d_wave_times);
+    (void)hipFree(c->d_sched);
     for (auto &p : c->events) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
@@ -365,7 +369,20 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     }
     EventPair &ev = c->events[c->events_used++];
     RTX_HIP(hipEventRecord(ev.start, c->stream));
-    hipError_t e = rtx::launch_render(p, c->stream);
+    const size_t npix = (size_t)rows * f.width;
+    if (c->sched_pixels < npix) {
+        RTX_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_sched);
+        c->d_sched = nullptr;
+        c->sched_pixels = 0;
+        RTX_HIP(hipMalloc(&c->d_sched, (2 * npix + 2 * rtx::kCostBuckets) * sizeof(uint32_t)));
+        c->sched_pixels = npix;
+    }
+    rtx::KSchedule sched;
+    sched.cost = c->d_sched;
+    sched.perm = c->d_sched + c->sched_pixels;
+    sched.buckets = c->d_sched + 2 * c->sched_pixels;
+    hipError_t e = rtx::launch_render(p, sched, c->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_render");
     RTX_HIP(hipEventRecord(ev.stop, c->stream));
     c->launches++;

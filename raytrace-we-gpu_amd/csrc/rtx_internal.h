@@ -43,7 +43,26 @@ struct KParams {
     float4 *accum;                 // progressive accumulation (NULL = plain frame)
     uint32_t accum_frames;         // frames in accum after this launch
     unsigned long long *wave_times;  // diagnostic: per-wave (start, end) s_memrealtime, or NULL
+    const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
+    uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
 };
+
+// Longest-processing-time-first scheduling for the persistent kernel: a
+// pre-pass traces kCostSpp samples per pixel and records their segment
+// count; a counting sort orders the pixel queue by that cost, descending,
+// so the pixels that take longest start first and the frame does not end
+// on a few expensive pixels started late.
+struct KSchedule {
+    uint32_t *cost;     // [npix]
+    uint32_t *perm;     // [npix]
+    uint32_t *buckets;  // [2 * kCostBuckets]: counts, cursors (zeroed per launch)
+};
+constexpr uint32_t kCostBuckets = 256;
+#ifndef RTX_LPT_SPP
+#define RTX_LPT_SPP 1
+#endif
+constexpr uint32_t kCostSpp = RTX_LPT_SPP;
+constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
 
 // LDS variant: spheres kept resident in LDS up to this count (16 B each);
 // larger scenes are streamed through LDS in chunks of kChunk spheres.
@@ -51,7 +70,7 @@ constexpr uint32_t kResidentMax = 4096;  // 64 KiB (+ 13 KiB candidate list)
 constexpr uint32_t kChunk = 1024;        // 16 KiB
 constexpr uint32_t kBlock = 256;         // 4 waves
 
-hipError_t launch_render(const KParams &p, hipStream_t stream);
+hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream);
 hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,
                                uint32_t height, uint32_t tile_rows, uint32_t nparts,
                                uint32_t max_rows, hipStream_t stream);

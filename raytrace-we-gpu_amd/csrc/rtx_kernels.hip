@@ -76,8 +76,8 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 #define RTX_BATCH 8
 #endif
 static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
-#ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a queue; 0: one pixel per lane
-#define RTX_PERSISTENT 0
+#ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a cost-ordered queue; 0: one pixel per lane
+#define RTX_PERSISTENT 1
 #endif
 #ifndef RTX_PRETEST  // 1: skip roots of spheres entirely behind the ray (exact, see below)
 #define RTX_PRETEST 0
@@ -94,20 +94,25 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_LISTMASK  // 1: one list entry per 4-sphere batch (index | 4-bit mask << 28)
 #define RTX_LISTMASK 1
 #endif
+#ifndef RTX_BLOCK  // threads per render workgroup (64 = one wave: freed slots refill independently)
+#define RTX_BLOCK 256
+#endif
+constexpr uint32_t kRB = RTX_BLOCK;
+static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64");
 #ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
 #define RTX_WAVES_PER_SIMD 0
 #endif
 #if RTX_WAVES_PER_SIMD
-#define RTX_RENDER_BOUNDS __launch_bounds__(kBlock, RTX_WAVES_PER_SIMD)
+#define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
 #else
-#define RTX_RENDER_BOUNDS __launch_bounds__(kBlock)
+#define RTX_RENDER_BOUNDS __launch_bounds__(kRB)
 #endif
 
 // Candidate list (RTX_DEFER): per lane kCand slots in LDS, slot-major
-// (slot j of lane t at [j * kBlock + t]: conflict-free), plus one dump slot
+// (slot j of lane t at [j * kRB + t]: conflict-free), plus one dump slot
 // that absorbs writes past the end (the lane then falls back, see below).
 constexpr int kCand = 12;
-constexpr uint32_t kListBytes = (kCand + 1) * kBlock * sizeof(uint32_t);  // 13,312 B
+constexpr uint32_t kListBytes = (kCand + 1) * kRB * sizeof(uint32_t);  // 13,312 B at 256
 static_assert(kListBytes % 16 == 0, "LDS carve must stay 16-byte aligned");
 
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
@@ -258,7 +263,7 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
                 for (int q = 0; q < RTX_BATCH; q += 4) {
                     const uint32_t m = (!(disc[q] < 0.0f) ? 1u : 0u) | (!(disc[q + 1] < 0.0f) ? 2u : 0u) |
                                        (!(disc[q + 2] < 0.0f) ? 4u : 0u) | (!(disc[q + 3] < 0.0f) ? 8u : 0u);
-                    my[min(cnt, (uint32_t)kCand) * kBlock] = (8 * b + h + q) | (m << 28);
+                    my[min(cnt, (uint32_t)kCand) * kRB] = (8 * b + h + q) | (m << 28);
                     cnt += m != 0u ? 1u : 0u;
                 }
 #else
@@ -266,7 +271,7 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
                 for (int k = 0; k < RTX_BATCH; ++k) {
                     // write unconditionally at the next free slot (or the
                     // dump slot), advance only for a candidate
-                    my[min(cnt, (uint32_t)kCand) * kBlock] = 8 * b + h + k;
+                    my[min(cnt, (uint32_t)kCand) * kRB] = 8 * b + h + k;
                     cnt += !(disc[k] < 0.0f) ? 1u : 0u;
                 }
 #endif
@@ -295,11 +300,11 @@ __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const
             const uint32_t bits = e >> 28;
             const uint32_t i = (e & 0x0fffffffu) + (uint32_t)__builtin_ctz(bits);
             e &= ~(1u << (28 + __builtin_ctz(bits)));
-            if ((e >> 28) == 0u && ++j < m) e = list[j * kBlock + threadIdx.x];
+            if ((e >> 28) == 0u && ++j < m) e = list[j * kRB + threadIdx.x];
 #else
     for (uint32_t j = 0; __ballot(j < m) != 0ull; ++j) {
         if (j < m) {
-            const uint32_t i = list[j * kBlock + threadIdx.x];
+            const uint32_t i = list[j * kRB + threadIdx.x];
 #endif
             const Ptr blk = soa + 32 * (i >> 3);
             const uint32_t q = i & 7u;
@@ -387,6 +392,10 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 // scatter, :207-252). Advances the lane to its next sample when the path
 // ends; clears `active` after the pixel's last sample.
 __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
+    if (P.cost_out) {  // scheduling pre-pass: one pixel per lane, record its segments
+        P.cost_out[L.gid] = L.segs;
+        return;
+    }
     // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
     f3 sum = L.acc;
     float n = (float)P.spp;
@@ -527,17 +536,18 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
     base = __shfl(base, leader, 64);
     if (!L.active) {
         const uint32_t g = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-        if (g < npix) start_pixel(P, F, g, L);
+        if (g < npix) start_pixel(P, F, P.perm ? P.perm[g] : g, L);
     }
     return base + cnt >= npix;
 }
 
 // Render kernel, per-wave independent: RTX_SRC 0 keeps the sphere blocks
 // resident in LDS (one copy per workgroup), 1 reads them with scalar loads.
-// RTX_PERSISTENT 1: the grid holds as many waves as the GPU keeps resident
-// and lanes pull pixels from the queue until it is exhausted; 0: exact grid,
-// one pixel per lane.
-__global__ void RTX_RENDER_BOUNDS k_render_persistent(const KParams P) {
+// kPersist: the grid holds as many waves as the GPU keeps resident and
+// lanes pull pixels from the (cost-ordered) queue until it is exhausted;
+// otherwise an exact grid, one pixel per lane.
+template <bool kPersist>
+__global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     // dynamic LDS: [candidate list, kListBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -547,7 +557,7 @@ __global__ void RTX_RENDER_BOUNDS k_render_persistent(const KParams P) {
     float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
-    for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kBlock) s_blk4[i] = g4[i];
+    for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kRB) s_blk4[i] = g4[i];
     __syncthreads();
 #else
     const cfloat_p soa = (cfloat_p)P.scene.soa;
@@ -558,16 +568,14 @@ __global__ void RTX_RENDER_BOUNDS k_render_persistent(const KParams P) {
     Lane L;
     L.active = false;
     L.segs = 0;
-#if RTX_PERSISTENT
-    bool exhausted = false;
+    bool exhausted = !kPersist;
+    if (!kPersist) {
+        const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
+        if (gid < npix) start_pixel(P, F, gid, L);
+    }
     for (;;) {
         if (!exhausted) exhausted = refill(P, F, npix, L);
         if (__ballot(L.active) == 0ull) break;  // spp, depth > 0: idle after refill => drained
-#else
-    const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
-    if (gid < npix) start_pixel(P, F, gid, L);
-    while (__ballot(L.active) != 0ull) {
-#endif
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
 #if RTX_SRC == 0
@@ -580,7 +588,7 @@ __global__ void RTX_RENDER_BOUNDS k_render_persistent(const KParams P) {
     }
     count_segments(P, L.segs);
     if (P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
-        const uint32_t w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+        const uint32_t w = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
         P.wave_times[2 * w] = t_start;
         P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -612,13 +620,89 @@ __global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
         for (uint32_t b0 = 0; b0 < nblk; b0 += kChunkBlk) {
             const uint32_t cnt = min(kChunkBlk, nblk - b0);
             __syncthreads();
-            for (uint32_t i = threadIdx.x; i < 8 * cnt; i += kBlock) s_blk4[i] = g4[8 * b0 + i];
+            for (uint32_t i = threadIdx.x; i < 8 * cnt; i += kRB) s_blk4[i] = g4[8 * b0 + i];
             __syncthreads();
             if (L.active) hit = hit_world(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit, list);
         }
         if (L.active) shade(P, F, L, min(hit, last), best);
     }
     count_segments(P, L.segs);
+}
+
+// ---- cost-ordered pixel queue (LPT scheduling, see KSchedule) ------------
+// One sample's segment count is a noisy estimate of a pixel's cost; the
+// key is the sum over a (2R+1)^2 window of neighbouring pixels (clamped
+// at the edges), which averages that noise over similar pixels.
+#ifndef RTX_LPT_RADIUS
+#define RTX_LPT_RADIUS 1
+#endif
+#ifndef RTX_LPT_CW  // extra weight of the centre pixel
+#define RTX_LPT_CW 0
+#endif
+__device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, uint32_t width, uint32_t rows) {
+    const int x = (int)(i % width), y = (int)(i / width);
+    uint32_t sum = 0;
+    for (int dy = -RTX_LPT_RADIUS; dy <= RTX_LPT_RADIUS; ++dy) {
+        const int yy = min(max(y + dy, 0), (int)rows - 1);
+        for (int dx = -RTX_LPT_RADIUS; dx <= RTX_LPT_RADIUS; ++dx) {
+            const int xx = min(max(x + dx, 0), (int)width - 1);
+            sum += cost[(uint32_t)yy * width + (uint32_t)xx];
+        }
+    }
+    sum += RTX_LPT_CW * cost[i];
+    return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
+}
+constexpr uint32_t kSortPerThread = 16;
+
+__global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
+                                                      uint32_t *counts) {
+    __shared__ uint32_t h[kCostBuckets];
+    for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
+    __syncthreads();
+    const uint32_t n = width * rows;
+    const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = base + k * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
+        if (h[b]) atomicAdd(&counts[b], h[b]);
+}
+
+// Positions: bucket start (prefix of the global counts) + a range the
+// block reserves in the bucket + the element's rank inside the block. The
+// order within a bucket is arbitrary; per-pixel results do not depend on it.
+__global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
+                                                         const uint32_t *counts, uint32_t *cursors,
+                                                         uint32_t *perm) {
+    __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
+    for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
+    __syncthreads();
+    const uint32_t n = width * rows;
+    const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
+    uint32_t rank[kSortPerThread], key[kSortPerThread];
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = base + k * kBlock + threadIdx.x;
+        key[k] = i < n ? cost_key(cost, i, width, rows) : 0u;
+        rank[k] = i < n ? atomicAdd(&h[key[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t pre = 0;
+        for (uint32_t b = 0; b < kCostBuckets; ++b) {
+            start[b] = pre;
+            pre += counts[b];
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
+        if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
+    __syncthreads();
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = base + k * kBlock + threadIdx.x;
+        if (i < n) perm[start[key[k]] + rank[k]] = i;
+    }
 }
 
 // spp == 0 or depth == 0: no segment is traced; the pixel is
@@ -647,11 +731,11 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
     img[i] = g[((uint64_t)part * max_rows + lr) * width + x];
 }
 
-__global__ void __launch_bounds__(kBlock) k_debug_hit_world(const KScene S, const float *rays,
+__global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const float *rays,
                                                             uint32_t nrays, float t_min,
                                                             float t_max, float *out) {
     __shared__ uint32_t list[kListBytes / sizeof(uint32_t)];
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t i = blockIdx.x * kRB + threadIdx.x;
     if (i >= nrays) return;
     const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
     const f3 d = mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
@@ -716,7 +800,7 @@ static uint32_t resident_blocks(const void *kern, size_t lds) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 1024;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)kBlock, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)kRB, lds) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return (uint32_t)(cus * per_cu);
@@ -728,28 +812,54 @@ static hipError_t allow_lds(const void *kern, size_t lds) {
     return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
-hipError_t launch_render(const KParams &p, hipStream_t stream) {
+hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
-    const uint32_t need = ceil_div(lanes, kBlock);
+    const uint32_t need = ceil_div(lanes, kRB);
     if (p.spp == 0 || p.depth == 0) {
-        hipLaunchKernelGGL(k_render_trivial, dim3(need), dim3(kBlock), 0, stream, p);
+        hipLaunchKernelGGL(k_render_trivial, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, p);
         return hipGetLastError();
     }
-    // Pixel queue head, zeroed on the stream ahead of the launch.
-    hipError_t e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
+    hipError_t e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
         const size_t lds = kListBytes + (RTX_SRC == 1 ? 0 : (size_t)p.scene.n_pad * sizeof(float4));
-        e = allow_lds((const void *)k_render_persistent, lds);
+        e = allow_lds((const void *)k_render<true>, lds);
+        if (e == hipSuccess) e = allow_lds((const void *)k_render<false>, lds);
         if (e != hipSuccess) return e;
-        const uint32_t blocks =
-            RTX_PERSISTENT ? min(need, resident_blocks((const void *)k_render_persistent, lds)) : need;
-        hipLaunchKernelGGL(k_render_persistent, dim3(blocks), dim3(kBlock), lds, stream, p);
+        if (!RTX_PERSISTENT || !sched.cost || p.spp < kLptMinSpp) {
+            hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, p);
+            return hipGetLastError();
+        }
+        // 1. cost pre-pass: kCostSpp samples per pixel, segments only
+        KParams c = p;
+        c.spp = min(p.spp, kCostSpp);
+        c.cost_out = sched.cost;
+        c.accum = nullptr;
+        c.counters = p.counters + 3;  // scratch: not part of the frame's segment count
+        c.wave_times = nullptr;
+        c.perm = nullptr;
+        e = hipMemsetAsync(sched.buckets, 0, 2 * kCostBuckets * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, c);
+        // 2. counting sort by cost, descending
+        const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
+        hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
+                           p.rows_local, sched.buckets);
+        hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
+                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
+        // 3. persistent render over the ordered queue
+        KParams q = p;
+        q.perm = sched.perm;
+        e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        const uint32_t blocks = min(need, resident_blocks((const void *)k_render<true>, lds));
+        hipLaunchKernelGGL(k_render<true>, dim3(blocks), dim3(kRB), lds, stream, q);
     } else {
         const size_t lds = kListBytes + kChunk * sizeof(float4);
+        e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
         const uint32_t blocks = min(need, resident_blocks((const void *)k_render_streamed, lds));
-        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kBlock), lds, stream, p);
+        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kRB), lds, stream, p);
     }
     return hipGetLastError();
 }
@@ -767,7 +877,7 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays, float t_min,
                                   float t_max, float *out, hipStream_t stream) {
     if (nrays == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kBlock)), dim3(kBlock), 0, stream, s,
+    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
                        rays, nrays, t_min, t_max, out);
     return hipGetLastError();
 }

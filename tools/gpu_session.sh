@@ -31,10 +31,12 @@ for s in $STEPS; do
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                 python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
-    variants) run variants 900 python tools/variant_bench.py --rounds 3 --frames 2 ;;
+    variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
     timeline) run timeline 300 python tools/wave_timeline.py ;;
-    c5)     run c5 900 python tools/variant_bench.py --rounds 2 --frames 1 --spp 16 --grid 159 --max-spheres 100000 $C5V ;;
+    vtimeline) for v in ${VTL:-blk64 lpt lpt_blk64}; do
+              run timeline_$v 300 python tools/wave_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_$v.so; done ;;
+    c5)     run c5 900 python tools/variant_bench.py --rounds 2 --frames 1 --spp 16 --grid 159 --max-spheres 100000 ${C5V:-} ;;
     diag)   run diag 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
                 SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/diag" -o run -- \
                 python3 bench.py --probe ;;

@@ -17,7 +17,7 @@ frame = rtx.camera_look_at(1920, 1080)
 ctx = rtx.Context(0, lib=lib)
 ctx.upload_world(world)
 ctx.set_frame(frame)
-W = (1920 * 1080 + 255) // 256 * 4
+W = (1920 * 1080 + 63) // 64  # upper bound on waves (any block size)
 ctx.arm_wave_times(W)
 ctx.render()
 ctx.sync()
@@ -29,7 +29,7 @@ dur = e - s
 T = e.max()
 grid = np.linspace(0, T, 200)
 resident = np.array([((s <= g) & (e > g)).sum() for g in grid])
-out = {"waves": int(len(t)), "kernel_us": float(T), "wave_us_mean": float(dur.mean()),
+out = {"lib": sys.argv[1] if len(sys.argv) > 1 else "default", "waves": int(len(t)), "kernel_us": float(T), "wave_us_mean": float(dur.mean()),
        "wave_us_p50": float(np.median(dur)), "wave_us_p99": float(np.percentile(dur, 99)),
        "wave_us_max": float(dur.max()), "mean_resident": float(resident.mean()),
        "peak_resident": int(resident.max()),
