@@ -45,9 +45,9 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := blk64 lpt lpt_s2 lpt_cw4 lpt_s2_cw4
-VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
-VFLAGS_blk64         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=64
+VARIANTS := best merge prof prof_merge
+VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8
+VFLAGS_blk64         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=0 -DRTX_BLOCK=64
 VFLAGS_blk128        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=128
 VFLAGS_blk64_w7      := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=64 -DRTX_WAVES_PER_SIMD=7
 VFLAGS_lpt           := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1
@@ -57,6 +57,17 @@ VFLAGS_lpt_r2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1
 VFLAGS_lpt_s2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2
 VFLAGS_lpt_cw4       := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_CW=4
 VFLAGS_lpt_s2_cw4    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2 -DRTX_LPT_CW=4
+VFLAGS_lpt_b1k       := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024
+VFLAGS_lpt_b1k_r2    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_RADIUS=2
+VFLAGS_lpt_b1k_cw4   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_CW=4
+VFLAGS_lpt_b1k_s2    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_SPP=2
+VFLAGS_lpt_coop4     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=4
+VFLAGS_lpt_coop8     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8
+VFLAGS_lpt_coop16    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=16
+VFLAGS_blk64_coop8   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=0 -DRTX_BLOCK=64 -DRTX_COOP_MAX=8
+VFLAGS_merge         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_SHADE_MERGE=1
+VFLAGS_prof          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_DIAG_PROF=1
+VFLAGS_prof_merge    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_DIAG_PROF=1 -DRTX_SHADE_MERGE=1
 VFLAGS_lpt_blk128    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_BLOCK=128
 VFLAGS_lds_stream_b8 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
 VDIR := $(LIBDIR)/variants
@@ -66,8 +77,8 @@ variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
 $(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS)
 	mkdir -p $(VDIR)/$*
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$*/k.o
-	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
-	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(VDIR)/$*/k.o $(VDIR)/$*/a.o $(VDIR)/$*/h.o
 
 .PHONY: variants

@@ -248,6 +248,12 @@ RTX_API int rtx_debug_math(rtx_ctx *ctx, int fn, const float *in0,
  * into a device buffer of that many waves (0 disarms); a call with the same
  * max_waves and host_pairs != NULL copies the pairs back (synchronous). */
 RTX_API int rtx_debug_wave_times(rtx_ctx *ctx, size_t max_waves, unsigned long long *host_pairs);
+/* Per-pixel cost diagnostic: traces the whole current frame with `spp`
+ * samples per pixel (0 = the world's spp), one lane per pixel, and writes
+ * each pixel's ray-segment count (hit_world calls) into host_cost
+ * (width * height uint32, row 0 = image bottom). Does not touch the
+ * framebuffer or the stats. Synchronous. */
+RTX_API int rtx_debug_pixel_cost(rtx_ctx *ctx, uint32_t spp, uint32_t *host_cost);
 
 #ifdef __cplusplus
 }

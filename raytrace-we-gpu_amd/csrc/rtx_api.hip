@@ -306,30 +306,10 @@ int rtx_accumulate(rtx_ctx *c, int reset) {
 
 uint32_t rtx_accumulated_frames(rtx_ctx *c) { return c ? c->accum_frames : 0; }
 
-static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
-                       float4 *accum, uint32_t accum_frames, uint32_t frame_index) {
-    if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_render_rows: no world uploaded");
-    if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_render_rows: no frame set");
-    if (tile_rows == 0 || nparts == 0 || part >= nparts)
-        return fail(RTX_ERR_INVALID, "rtx_render_rows: bad partition");
-    int rc = set_device(c);
-    if (rc) return rc;
+static rtx::KParams make_params(const rtx_ctx *c, uint32_t rows, uint32_t tile_rows, uint32_t part,
+                                uint32_t nparts, float4 *out, float4 *accum, uint32_t accum_frames,
+                                uint32_t frame_index) {
     const rtx_frame &f = c->frame;
-    const uint32_t rows = rtx_part_rows(f.height, tile_rows, part, nparts);
-    float4 *out = reinterpret_cast<float4 *>(d_out);
-    if (!out) {
-        if (nparts != 1) return fail(RTX_ERR_INVALID, "rtx_render_rows: d_out NULL needs nparts == 1");
-        const size_t px = (size_t)f.width * f.height;
-        if (c->fb_pixels != px) {
-            RTX_HIP(hipStreamSynchronize(c->stream));
-            (void)hipFree(c->d_fb);
-            c->d_fb = nullptr;
-            c->fb_pixels = 0;
-            RTX_HIP(hipMalloc(&c->d_fb, px * sizeof(float4)));
-            c->fb_pixels = px;
-        }
-        out = c->d_fb;
-    }
     rtx::KParams p{};
     p.scene = scene_of(c);
     p.out = out;
@@ -360,6 +340,34 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     }
     p.img_w = f.img_w;
     p.img_h = f.img_h;
+    return p;
+}
+
+static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
+                       float4 *accum, uint32_t accum_frames, uint32_t frame_index) {
+    if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_render_rows: no world uploaded");
+    if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_render_rows: no frame set");
+    if (tile_rows == 0 || nparts == 0 || part >= nparts)
+        return fail(RTX_ERR_INVALID, "rtx_render_rows: bad partition");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const rtx_frame &f = c->frame;
+    const uint32_t rows = rtx_part_rows(f.height, tile_rows, part, nparts);
+    float4 *out = reinterpret_cast<float4 *>(d_out);
+    if (!out) {
+        if (nparts != 1) return fail(RTX_ERR_INVALID, "rtx_render_rows: d_out NULL needs nparts == 1");
+        const size_t px = (size_t)f.width * f.height;
+        if (c->fb_pixels != px) {
+            RTX_HIP(hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_fb);
+            c->d_fb = nullptr;
+            c->fb_pixels = 0;
+            RTX_HIP(hipMalloc(&c->d_fb, px * sizeof(float4)));
+            c->fb_pixels = px;
+        }
+        out = c->d_fb;
+    }
+    rtx::KParams p = make_params(c, rows, tile_rows, part, nparts, out, accum, accum_frames, frame_index);
 
     if (c->events_used == c->events.size()) {
         EventPair ev;
@@ -382,6 +390,8 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     sched.cost = c->d_sched;
     sched.perm = c->d_sched + c->sched_pixels;
     sched.buckets = c->d_sched + 2 * c->sched_pixels;
+    sched.npix = (uint32_t)c->sched_pixels;
+    sched.nbuckets = rtx::kCostBuckets;
     hipError_t e = rtx::launch_render(p, sched, c->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_render");
     RTX_HIP(hipEventRecord(ev.stop, c->stream));
@@ -502,6 +512,28 @@ int rtx_copy_to_device(rtx_ctx *c, void *d_dst, const void *host, size_t bytes) 
     if (rc) return rc;
     RTX_HIP(hipMemcpyAsync(d_dst, host, bytes, hipMemcpyHostToDevice, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+int rtx_debug_pixel_cost(rtx_ctx *c, uint32_t spp, uint32_t *host_cost) {
+    if (!c || !host_cost) return fail(RTX_ERR_INVALID, "rtx_debug_pixel_cost: null argument");
+    if (!c->have_world || !c->have_frame) return fail(RTX_ERR_STATE, "rtx_debug_pixel_cost: no world/frame");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const rtx_frame &f = c->frame;
+    const size_t npix = (size_t)f.width * f.height;
+    uint32_t *d = nullptr;
+    RTX_HIP(hipMalloc(&d, npix * sizeof(uint32_t)));
+    rtx::KParams p = make_params(c, f.height, 1, 0, 1, nullptr, nullptr, 0, f.frame_index);
+    if (spp) p.spp = spp;
+    p.cost_out = d;
+    p.counters = c->d_counters + 3;
+    p.wave_times = nullptr;
+    hipError_t e = rtx::launch_cost(p, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(host_cost, d, npix * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "rtx_debug_pixel_cost");
     return RTX_OK;
 }
 

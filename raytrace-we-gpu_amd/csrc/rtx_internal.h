@@ -55,9 +55,14 @@ struct KParams {
 struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
-    uint32_t *buckets;  // [2 * kCostBuckets]: counts, cursors (zeroed per launch)
+    uint32_t *buckets;  // [2 * nbuckets]: counts, cursors (zeroed per launch)
+    uint32_t npix;      // capacity of cost / perm
+    uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
 };
-constexpr uint32_t kCostBuckets = 256;
+#ifndef RTX_LPT_BUCKETS
+#define RTX_LPT_BUCKETS 256
+#endif
+constexpr uint32_t kCostBuckets = RTX_LPT_BUCKETS;
 #ifndef RTX_LPT_SPP
 #define RTX_LPT_SPP 1
 #endif
@@ -71,6 +76,7 @@ constexpr uint32_t kChunk = 1024;        // 16 KiB
 constexpr uint32_t kBlock = 256;         // 4 waves
 
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream);
+hipError_t launch_cost(const KParams &p, hipStream_t stream);  // exact grid, p.cost_out set
 hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,
                                uint32_t height, uint32_t tile_rows, uint32_t nparts,
                                uint32_t max_rows, hipStream_t stream);

@@ -76,6 +76,15 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 #define RTX_BATCH 8
 #endif
 static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
+#ifndef RTX_COOP_MAX  // tail mode: a wave with <= this many active lanes traces their rays together
+#define RTX_COOP_MAX 8
+#endif
+#ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
+#define RTX_DIAG_PROF 0
+#endif
+#ifndef RTX_SHADE_MERGE  // 1: Lambert and metal lanes share one scatter path
+#define RTX_SHADE_MERGE 1
+#endif
 #ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a cost-ordered queue; 0: one pixel per lane
 #define RTX_PERSISTENT 1
 #endif
@@ -114,6 +123,23 @@ static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64"
 constexpr int kCand = 12;
 constexpr uint32_t kListBytes = (kCand + 1) * kRB * sizeof(uint32_t);  // 13,312 B at 256
 static_assert(kListBytes % 16 == 0, "LDS carve must stay 16-byte aligned");
+
+#if RTX_DIAG_PROF
+// Diagnostic event counters, one set per wave in LDS: [0] batches scanned
+// [1] batches recorded (some lane had a candidate) [2] resolve iterations
+// [3] lanes falling back to the in-order scan [4] candidate entries (lanes)
+__device__ __forceinline__ uint32_t *diag_slots() {
+    __shared__ uint32_t s[kRB / 64][8];
+    return s[threadIdx.x / 64];
+}
+__device__ __forceinline__ void diag_add(int k, uint32_t v) {
+    const uint64_t m = __ballot(1);
+    if ((int)(threadIdx.x & 63u) == __ffsll((long long)m) - 1) diag_slots()[k] += v;
+}
+#define RTX_DIAG_ADD(k, v) diag_add(k, v)
+#else
+#define RTX_DIAG_ADD(k, v)
+#endif
 
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
 // the near one is outside [t_min, best] (Sphere.cpp:15-24); strict
@@ -257,7 +283,9 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
             for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
             any = __ballot(!(m < 0.0f));
 #endif
+            RTX_DIAG_ADD(0, 1u);
             if (any != 0ull) {
+                RTX_DIAG_ADD(1, 1u);
 #if RTX_LISTMASK
 #pragma unroll
                 for (int q = 0; q < RTX_BATCH; q += 4) {
@@ -293,9 +321,11 @@ __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const
 #if RTX_LISTMASK
     uint32_t j = 0, e = 0;  // entry index, remaining mask bits of entry j
     if (m) e = list[threadIdx.x];
+    RTX_DIAG_ADD(4, (uint32_t)__popcll(__ballot(m != 0u)));
     for (;;) {
         const bool live = j < m;
         if (__ballot(live) == 0ull) break;
+        RTX_DIAG_ADD(2, 1u);
         if (live) {
             const uint32_t bits = e >> 28;
             const uint32_t i = (e & 0x0fffffffu) + (uint32_t)__builtin_ctz(bits);
@@ -341,6 +371,7 @@ __device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, 
     const int idx0 = idx;
     const uint32_t cnt = scan_candidates(soa, nblk, o, d, a, list);
     if (!resolve_candidates(soa, blk0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
+        RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
         idx = hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx0);
     }
@@ -351,6 +382,63 @@ __device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, 
 #endif
 }
 
+// ---- wave-cooperative hit_world (frame tail) ------------------------------
+__device__ __forceinline__ float read_lane(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+
+// ONE wave-uniform ray against all n spheres: lane l takes spheres l, l+64,
+// ... with the arithmetic of resolve_candidates, keeps its own (min c,
+// largest index) and the wave reduces the 64 results — the same
+// order-independent rule, hence the in-order scan's answer (see above).
+// Any non-finite root sets `seq`: the caller redoes the ray with hit_world.
+__device__ __forceinline__ int hit_world_coop(const float *soa, uint32_t n, f3 o, f3 d, float a,
+                                              float inv_a, float t_min, float &best, bool &seq) {
+    const float inf = __uint_as_float(0x7f800000u);
+    float bc = inf;
+    int bg = -1;
+    bool bad = false;
+#pragma unroll 2
+    for (uint32_t i = threadIdx.x & 63u; i < n; i += 64u) {
+        const float *blk = soa + 32 * (i >> 3);
+        const uint32_t q = i & 7u;
+        const float ocx = o.x - blk[q];
+        const float ocy = o.y - blk[8 + q];
+        const float ocz = o.z - blk[16 + q];
+        const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + q])));
+        const float disc = fmaf(hb, hb, -(a * cc));
+        if (!(disc < 0.0f)) {
+            const float sq = sqrtf(disc);
+            const float rn = (-hb - sq) * inv_a;
+            const float rf = (-hb + sq) * inv_a;
+            if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) bad = true;
+            const bool use_n = !(rn < t_min);
+            const float c = use_n ? rn : rf;
+            if ((use_n || !(rf < t_min)) && (c < bc || (c == bc && (int)i > bg))) {
+                bc = c;
+                bg = (int)i;
+            }
+        }
+    }
+    seq = __ballot(bad) != 0ull;
+    if (seq) return -1;
+    // c >= t_min > 0: its bits order like its value; ties -> larger index
+    uint64_t key = bg >= 0 ? ((uint64_t)__float_as_uint(bc) << 32) | (uint64_t)(0xffffffffu - (uint32_t)bg)
+                           : ~0ull;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, s, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), s, 64);
+        const uint64_t other = ((uint64_t)hi << 32) | lo;
+        key = other < key ? other : key;
+    }
+    if (key == ~0ull) return -1;
+    const float c = __uint_as_float((uint32_t)(key >> 32));
+    if (!(c <= best)) return -1;  // accepted iff c <= t_max (c < best, or c == best and index > -1)
+    best = c;
+    return (int)(0xffffffffu - (uint32_t)key);
+}
 
 // Lane state: the pixel it is tracing and that pixel's current path.
 struct Lane {
@@ -431,6 +519,17 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
         const float4 mv = S.mval[hit];
         f3 dir;
         bool scattered = true;
+#if RTX_SHADE_MERGE
+        // Lambert and metal share random_in_unit_sphere and normalize: run
+        // them once for both kinds of lane (same ops per lane as below).
+        if (mt == 0 || mt == 1) {
+            const f3 rius = random_in_unit_sphere(L.seed);
+            const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
+                                 : reflect3(L.d, nrm) + mv.w * rius;     // METAL (:219-227)
+            dir = normalize3(v);
+            L.col = L.col * mk3(mv.x, mv.y, mv.z);
+        } else if (mt == 2) {
+#else
         if (mt == 0) {  // DIFFUSE (:209-217)
             const f3 rius = random_in_unit_sphere(L.seed);
             const f3 target = (p + nrm) + rius;
@@ -441,7 +540,9 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
             const f3 rius = random_in_unit_sphere(L.seed);
             dir = normalize3(refl + mv.w * rius);
             L.col = L.col * mk3(mv.x, mv.y, mv.z);
-        } else if (mt == 2) {  // DIELECTRIC (:229-249), atten = 1
+        } else if (mt == 2) {
+#endif
+            // DIELECTRIC (:229-249), atten = 1
             const float ratio = ff ? (1.0f / mv.w) : mv.w;
             const f3 ud = normalize3(L.d);
             const float cosine = fminf(dot3(-ud, nrm), 1.0f);
@@ -573,9 +674,67 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
         if (gid < npix) start_pixel(P, F, gid, L);
     }
+#if RTX_DIAG_PROF
+    // [0] refill clocks [1] hit_world [2] shade [3] tail mode [4] iterations [5] tail iterations
+    // [6] active lanes summed over iterations
+    unsigned long long pr[7] = {0, 0, 0, 0, 0, 0, 0};
+    if ((threadIdx.x & 63u) == 0u)
+        for (int k = 0; k < 8; ++k) diag_slots()[k] = 0u;
+    unsigned long long tq = __builtin_readcyclecounter();
+#define RTX_PROF(k)                                          \
+    {                                                        \
+        const unsigned long long tn = __builtin_readcyclecounter(); \
+        pr[k] += tn - tq;                                    \
+        tq = tn;                                             \
+    }
+#else
+#define RTX_PROF(k)
+#endif
     for (;;) {
         if (!exhausted) exhausted = refill(P, F, npix, L);
-        if (__ballot(L.active) == 0ull) break;  // spp, depth > 0: idle after refill => drained
+        const uint64_t act = __ballot(L.active);
+        RTX_PROF(0)
+        if (act == 0ull) break;  // spp, depth > 0: idle after refill => drained
+#if RTX_DIAG_PROF
+        pr[4]++;
+        pr[6] += __popcll(act);
+#endif
+#if RTX_SRC == 1
+        if (RTX_COOP_MAX && exhausted && __popcll(act) <= RTX_COOP_MAX) {
+#if RTX_DIAG_PROF
+            pr[5]++;
+#endif
+            // Frame tail: the few pixels left in this wave are its critical
+            // path; trace their rays one after another, each across all 64
+            // lanes, instead of all of them on one lane each.
+            float my_best = __uint_as_float(0x7f800000u);
+            int my_hit = -1;
+            bool my_seq = false;
+            for (uint64_t m = act; m != 0ull; m &= m - 1ull) {
+                const int src = __ffsll((long long)m) - 1;
+                const f3 ro = mk3(read_lane(L.o.x, src), read_lane(L.o.y, src), read_lane(L.o.z, src));
+                const f3 rd = mk3(read_lane(L.d.x, src), read_lane(L.d.y, src), read_lane(L.d.z, src));
+                float b = __uint_as_float(0x7f800000u);
+                bool seq = false;
+                const int h = hit_world_coop(P.scene.soa, P.scene.n, ro, rd, read_lane(L.a, src),
+                                             read_lane(L.inv_a, src), kTMin, b, seq);
+                if ((int)(threadIdx.x & 63u) == src) {
+                    my_best = b;
+                    my_hit = h;
+                    my_seq = seq;
+                }
+            }
+            if (L.active) {
+                if (my_seq) {
+                    my_best = __uint_as_float(0x7f800000u);
+                    my_hit = hit_world(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, my_best, -1, list);
+                }
+                shade(P, F, L, min(my_hit, last), my_best);
+            }
+            RTX_PROF(3)
+            continue;
+        }
+#endif
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
 #if RTX_SRC == 0
@@ -583,11 +742,19 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #else
             const int hit = hit_world(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
 #endif
+            RTX_PROF(1)
             shade(P, F, L, min(hit, last), best);
         }
+        RTX_PROF(2)
     }
+#if RTX_DIAG_PROF
+    if (P.wave_times && (threadIdx.x & 63u) == 0u)
+        for (int k = 0; k < 7; ++k) atomicAdd(&P.wave_times[k], pr[k]);
+    if (P.wave_times && (threadIdx.x & 63u) == 0u)
+        for (int k = 0; k < 5; ++k) atomicAdd(&P.wave_times[8 + k], (unsigned long long)diag_slots()[k]);
+#endif
     count_segments(P, L.segs);
-    if (P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
+    if (!RTX_DIAG_PROF && P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
         const uint32_t w = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
         P.wave_times[2 * w] = t_start;
         P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
@@ -812,6 +979,17 @@ static hipError_t allow_lds(const void *kern, size_t lds) {
     return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
+hipError_t launch_cost(const KParams &p, hipStream_t stream) {
+    const uint64_t lanes = (uint64_t)p.rows_local * p.width;
+    if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
+    if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
+    const size_t lds = kListBytes + (RTX_SRC == 1 ? 0 : (size_t)p.scene.n_pad * sizeof(float4));
+    hipError_t e = allow_lds((const void *)k_render<false>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_render<false>, dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
@@ -830,6 +1008,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
             hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, p);
             return hipGetLastError();
         }
+        if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
         // 1. cost pre-pass: kCostSpp samples per pixel, segments only
         KParams c = p;
         c.spp = min(p.spp, kCostSpp);

@@ -105,6 +105,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_debug_hit_world": (C.c_int, [ctx, f, u32, C.c_float, C.c_float, f]),
         "rtx_debug_math": (C.c_int, [ctx, C.c_int, f, f, u32, f]),
         "rtx_debug_wave_times": (C.c_int, [ctx, C.c_size_t, C.POINTER(C.c_uint64)]),
+        "rtx_debug_pixel_cost": (C.c_int, [ctx, u32, C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -327,6 +328,14 @@ class Context:
         out = np.zeros((max_waves, 2), np.uint64)
         _check(self._lib.rtx_debug_wave_times(self._h, max_waves, out.ctypes.data_as(C.POINTER(C.c_uint64))),
                "rtx_debug_wave_times", self._lib)
+        return out
+
+    def debug_pixel_cost(self, spp: int = 0) -> np.ndarray:
+        """Per-pixel ray-segment counts of the current frame, (H, W) uint32."""
+        f = self.frame
+        out = np.zeros((f.height, f.width), np.uint32)
+        _check(self._lib.rtx_debug_pixel_cost(self._h, spp, out.ctypes.data_as(C.POINTER(C.c_uint32))),
+               "rtx_debug_pixel_cost", self._lib)
         return out
 
     def debug_math(self, fn: str, in0: np.ndarray, in1: Optional[np.ndarray] = None) -> np.ndarray:

@@ -215,6 +215,30 @@ def test_determinism(gpu_ctx, rtx):
     assert_bits_equal(a, b, "two renders")
 
 
+def test_lpt_schedule_and_pixel_cost(gpu_ctx, oracle, rtx):
+    """spp >= 8 takes the cost-ordered persistent path (1-spp pre-pass +
+    counting sort): the frame and segment count equal the oracle's, and the
+    per-pixel segment counts (rtx_debug_pixel_cost) equal the oracle's
+    per-row totals and sum to the frame's count."""
+    W, H = 128, 72
+    world = rtx.random_world(11, depth=50, spp=9)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(H), nthreads=8)
+    assert_bits_equal(img, want, "LPT frame")
+    assert st.segments == segs
+    cost = gpu_ctx.debug_pixel_cost(0)
+    assert cost.shape == (H, W) and int(cost.sum()) == segs
+    for y in (0, 31, H - 1):
+        _, row_segs = oracle.render_rows(world, frame, [y])
+        assert int(cost[y].sum()) == row_segs
+    one = gpu_ctx.debug_pixel_cost(1)
+    assert (one >= 1).all() and (one <= 50).all()
+    # the pre-pass does not disturb the framebuffer or the stats
+    assert_bits_equal(gpu_ctx.download(), img, "framebuffer after cost pass")
+    assert gpu_ctx.stats().segments == segs
+
+
 # ---------------------------------------------------------------------------
 # row-tile partitions (the multi-GPU data path) on one device
 # ---------------------------------------------------------------------------
