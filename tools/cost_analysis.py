@@ -29,15 +29,20 @@ ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--grid", type=int, default=11)
 ap.add_argument("--lanes", type=int, default=6144 * 64)
 ap.add_argument("--out", default="")
+ap.add_argument("--from-npz", default="", help="analyse a saved cost.npz (no GPU)")
 a = ap.parse_args()
 
-world = rtx.random_world(a.grid, depth=50, spp=a.spp)
-frame = rtx.camera_look_at(a.width, a.height, aspect=a.width / a.height)
-c = rtx.Context(0)
-c.upload_world(world)
-c.set_frame(frame)
-full = c.debug_pixel_cost(0).astype(np.int64)
-one = c.debug_pixel_cost(1).astype(np.int64)
+if a.from_npz:
+    d = np.load(a.from_npz)
+    full, one = d["full"].astype(np.int64), d["one"].astype(np.int64)
+else:
+    world = rtx.random_world(a.grid, depth=50, spp=a.spp)
+    frame = rtx.camera_look_at(a.width, a.height, aspect=a.width / a.height)
+    c = rtx.Context(0)
+    c.upload_world(world)
+    c.set_frame(frame)
+    full = c.debug_pixel_cost(0).astype(np.int64)
+    one = c.debug_pixel_cost(1).astype(np.int64)
 if a.out:
     np.savez_compressed(a.out, full=full.astype(np.uint32), one=one.astype(np.uint32))
 
@@ -63,7 +68,7 @@ def makespan(costs_in_order, lanes):
 flat = full.ravel()
 total = int(flat.sum())
 R = a.lanes
-bound = max(total / R, flat.max())
+bound = float(max(total / R, flat.max()))
 rep = {"pixels": int(flat.size), "segments": total, "mean": float(flat.mean()),
        "p50": float(np.percentile(flat, 50)), "p99": float(np.percentile(flat, 99)),
        "p999": float(np.percentile(flat, 99.9)), "max": int(flat.max()),
