@@ -11,7 +11,7 @@ BINDIR    := $(PKG)/bin
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function
 LIB       := $(LIBDIR)/librtx.so
 CLI       := $(BINDIR)/rtx_cli
-HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h
+HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)/rtx_prefilter.h
 
 all: $(LIB) $(CLI) oracle
 
@@ -45,7 +45,9 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best merge prof prof_merge
+VARIANTS := best pre0 prof pre0_prof
+VFLAGS_pre0          := -DRTX_PREFILTER=0
+VFLAGS_pre0_prof     := -DRTX_PREFILTER=0 -DRTX_DIAG_PROF=1
 VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8
 VFLAGS_blk64         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=0 -DRTX_BLOCK=64
 VFLAGS_blk128        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=128

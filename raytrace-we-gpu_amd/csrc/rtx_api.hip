@@ -7,6 +7,8 @@
 // float4 framebuffer, Dispatch becomes rtx_render_rows.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -15,6 +17,7 @@
 
 #include "../../include/rtx.h"
 #include "rtx_internal.h"
+#include "rtx_prefilter.h"
 
 namespace {
 
@@ -47,6 +50,8 @@ struct rtx_ctx {
     hipStream_t stream = nullptr;  // own_stream or an external one
     // scene (device)
     float *d_soa = nullptr;
+    float *d_pre = nullptr;  // prefilter blocks (rtx_prefilter.h)
+    float smag = 0.0f;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
@@ -84,10 +89,12 @@ int set_device(rtx_ctx *c) {
 
 void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_soa);
+    (void)hipFree(c->d_pre);
     (void)hipFree(c->d_cen);
     (void)hipFree(c->d_mtype);
     (void)hipFree(c->d_mval);
     c->d_soa = nullptr;
+    c->d_pre = nullptr;
     c->d_cen = nullptr;
     c->d_mtype = nullptr;
     c->d_mval = nullptr;
@@ -97,6 +104,8 @@ void free_world(rtx_ctx *c) {
 rtx::KScene scene_of(const rtx_ctx *c) {
     rtx::KScene s;
     s.soa = c->d_soa;
+    s.pre = c->d_pre;
+    s.smag = c->smag;
     s.cen = c->d_cen;
     s.mtype = c->d_mtype;
     s.mval = c->d_mval;
@@ -199,11 +208,15 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
                 return fail(RTX_ERR_INVALID, "rtx_upload_world: sphere " + std::to_string(i) +
                                                  " has a non-finite or |value| > 1e15 component");
         }
+    // The prefiltered scan's list entries hold a 24-bit local sphere index.
+    if (w->count > (1u << 24) - rtx::kPad)
+        return fail(RTX_ERR_INVALID, "rtx_upload_world: more than 16,777,208 spheres");
     int rc = set_device(c);
     if (rc) return rc;
     const uint32_t n = w->count;
     const uint32_t n_pad = (n + rtx::kPad - 1) / rtx::kPad * rtx::kPad;
-    std::vector<float> soa(4 * (size_t)n_pad);
+    std::vector<float> soa(4 * (size_t)n_pad), pre(4 * (size_t)n_pad);
+    double smag = 0.0;  // max |c| + |r|, for the prefilter's overflow guard
     std::vector<float4> cen(n), mval(n);
     std::vector<int> mtype(n);
     for (uint32_t i = 0; i < n_pad; ++i) {
@@ -214,8 +227,18 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         blk[i % 8] = w->spheres[4 * k + 0];
         blk[8 + i % 8] = w->spheres[4 * k + 1];
         blk[16 + i % 8] = w->spheres[4 * k + 2];
-        blk[24 + i % 8] = -(r * r);
+        const float r2 = r * r;
+        blk[24 + i % 8] = -r2;
+        float *pb = &pre[32 * (size_t)(i / 8)];
+        pb[i % 8] = blk[i % 8];
+        pb[8 + i % 8] = blk[8 + i % 8];
+        pb[16 + i % 8] = blk[16 + i % 8];
+        pb[24 + i % 8] = rtx::prefilter_R(blk[i % 8], blk[8 + i % 8], blk[16 + i % 8], r2);
+        const double cx = blk[i % 8], cy = blk[8 + i % 8], cz = blk[16 + i % 8];
+        smag = std::max(smag, std::sqrt(cx * cx + cy * cy + cz * cz) + std::fabs((double)r));
     }
+    float smag_f = (float)smag;
+    if ((double)smag_f < smag) smag_f = std::nextafter(smag_f, INFINITY);
     for (uint32_t i = 0; i < n; ++i) {
         cen[i] = make_float4(w->spheres[4 * i + 0], w->spheres[4 * i + 1], w->spheres[4 * i + 2],
                              w->spheres[4 * i + 3]);
@@ -230,6 +253,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     free_world(c);
     const size_t cap = n ? n : 1;
     RTX_HIP(hipMalloc(&c->d_soa, (n_pad ? 4 * (size_t)n_pad : 4) * sizeof(float)));
+    RTX_HIP(hipMalloc(&c->d_pre, (n_pad ? 4 * (size_t)n_pad : 4) * sizeof(float)));
     RTX_HIP(hipMalloc(&c->d_cen, cap * sizeof(float4)));
     RTX_HIP(hipMalloc(&c->d_mtype, cap * sizeof(int)));
     RTX_HIP(hipMalloc(&c->d_mval, cap * sizeof(float4)));
@@ -237,6 +261,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     // order against the legacy null stream), then wait for them.
     if (n) {
         RTX_HIP(hipMemcpyAsync(c->d_soa, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_pre, pre.data(), pre.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cen, cen.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -245,6 +270,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (c->n != n) c->n_changed = true;
     c->n = n;
     c->n_pad = n_pad;
+    c->smag = smag_f;
     c->depth = w->depth;
     c->spp = w->spp;
     c->have_world = true;

@@ -17,12 +17,19 @@ namespace rtx {
 // `soa` is padded to n_pad = roundup(n, kPad) spheres with copies of sphere
 // n-1; a padded copy can only win where sphere n-1 itself would (same data,
 // later index wins ties), so kernels clamp the winning index to n-1.
+//   pre   float[n_pad*4]  AoSoA-8 like soa: cx[8] cy[8] cz[8] R[8], R the
+//                         prefilter's inflated r^2 (rtx_prefilter.h) — the
+//                         array every ray segment scans
+// `smag` bounds |c| + r over the scene (rounded up), for the prefilter's
+// per-ray overflow guard.
 struct KScene {
     const float *soa;
+    const float *pre;
     const float4 *cen;
     const int *mtype;
     const float4 *mval;
     uint32_t n, n_pad;
+    float smag;
 };
 
 constexpr uint32_t kPad = 8;  // spheres per AoSoA block

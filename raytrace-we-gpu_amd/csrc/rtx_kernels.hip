@@ -28,6 +28,7 @@
 //    accepted one.
 #include "rtx_device_math.h"
 #include "rtx_internal.h"
+#include "rtx_prefilter.h"
 
 namespace rtx {
 
@@ -102,6 +103,9 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #endif
 #ifndef RTX_LISTMASK  // 1: one list entry per 4-sphere batch (index | 4-bit mask << 28)
 #define RTX_LISTMASK 1
+#endif
+#ifndef RTX_PREFILTER  // 1: scan with the line-distance prefilter (rtx_prefilter.h; RTX_SRC 1 only)
+#define RTX_PREFILTER 1
 #endif
 #ifndef RTX_BLOCK  // threads per render workgroup (64 = one wave: freed slots refill independently)
 #define RTX_BLOCK 256
@@ -310,8 +314,11 @@ __device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o
 }
 
 // Resolve the lane's candidates (local indices into `soa`, global index =
-// 8*blk0 + local). Returns false if the lane must fall back.
-template <typename Ptr>
+// 8*blk0 + local). List entries are `first local index | mask << kSh`.
+// A candidate whose exact disc is < 0 (a prefilter false positive) is
+// skipped, as the reference's `if (d < 0) return false`. Returns false if
+// the lane must fall back.
+template <int kSh, typename Ptr>
 __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const uint32_t *list,
                                                    uint32_t cnt, f3 o, f3 d, float a, float inv_a,
                                                    float t_min, float &best, int &idx) {
@@ -327,10 +334,10 @@ __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const
         if (__ballot(live) == 0ull) break;
         RTX_DIAG_ADD(2, 1u);
         if (live) {
-            const uint32_t bits = e >> 28;
-            const uint32_t i = (e & 0x0fffffffu) + (uint32_t)__builtin_ctz(bits);
-            e &= ~(1u << (28 + __builtin_ctz(bits)));
-            if ((e >> 28) == 0u && ++j < m) e = list[j * kRB + threadIdx.x];
+            const uint32_t k = (uint32_t)__builtin_ctz(e >> kSh);
+            const uint32_t i = (e & ((1u << kSh) - 1u)) + k;
+            e &= ~(1u << (kSh + k));
+            if ((e >> kSh) == 0u && ++j < m) e = list[j * kRB + threadIdx.x];
 #else
     for (uint32_t j = 0; __ballot(j < m) != 0ull; ++j) {
         if (j < m) {
@@ -344,16 +351,18 @@ __device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const
             const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
             const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + q])));
             const float disc = fmaf(hb, hb, -(a * cc));
-            const float sq = sqrtf(disc);
-            const float rn = (-hb - sq) * inv_a;
-            const float rf = (-hb + sq) * inv_a;
-            if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) ok = false;
-            const bool use_n = !(rn < t_min);
-            const float c = use_n ? rn : rf;
-            const int g = (int)(8 * blk0 + i);
-            if ((use_n || !(rf < t_min)) && (c < best || (c == best && g > idx))) {
-                best = c;
-                idx = g;
+            if (!(disc < 0.0f)) {
+                const float sq = sqrtf(disc);
+                const float rn = (-hb - sq) * inv_a;
+                const float rf = (-hb + sq) * inv_a;
+                if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) ok = false;
+                const bool use_n = !(rn < t_min);
+                const float c = use_n ? rn : rf;
+                const int g = (int)(8 * blk0 + i);
+                if ((use_n || !(rf < t_min)) && (c < best || (c == best && g > idx))) {
+                    best = c;
+                    idx = g;
+                }
             }
         }
     }
@@ -370,7 +379,7 @@ __device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, 
     const float best0 = best;
     const int idx0 = idx;
     const uint32_t cnt = scan_candidates(soa, nblk, o, d, a, list);
-    if (!resolve_candidates(soa, blk0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
+    if (!resolve_candidates<28>(soa, blk0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
         idx = hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx0);
@@ -379,6 +388,89 @@ __device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, 
 #else
     (void)list;
     return hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx);
+#endif
+}
+
+#if RTX_PREFILTER
+// ---- prefiltered scan (rtx_prefilter.h) -----------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Q = R - pu^2 - pv^2 for sphere pairs (v_pk_fma_f32), 8 spheres per step
+// from the `pre` blocks; one max + ballot skips a step in which no lane's
+// line comes near any of the 8. A lane with flagged spheres appends ONE
+// entry per 8-sphere block: local index of the block's first sphere |
+// 8-bit mask << 24 (so n_pad <= 2^24, checked at upload).
+__device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t nblk, const LineTest &T,
+                                                   uint32_t *list) {
+    uint32_t cnt = 0;
+    uint32_t *my = list + threadIdx.x;
+    const f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
+    const f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const cfloat_p blk = pre + 32 * b;
+        f2v q[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const f2v cx = {blk[2 * p], blk[2 * p + 1]};
+            const f2v cy = {blk[8 + 2 * p], blk[9 + 2 * p]};
+            const f2v cz = {blk[16 + 2 * p], blk[17 + 2 * p]};
+            const f2v R = {blk[24 + 2 * p], blk[25 + 2 * p]};
+            const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
+            const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
+            q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+        }
+        const float mx = fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), fmaxf(q[1].x, q[1].y)),
+                               fmaxf(fmaxf(q[2].x, q[2].y), fmaxf(q[3].x, q[3].y)));
+        RTX_DIAG_ADD(0, 1u);
+        if (__ballot(!(mx < T.thr)) != 0ull) {
+            RTX_DIAG_ADD(1, 1u);
+            // q - thr >= +0 exactly when q >= thr (q is finite; thr = -inf
+            // gives +inf): the sign bits, shifted in from sphere 7 down to
+            // sphere 0, are the NOT-flagged mask.
+            uint32_t inv = 0;
+#pragma unroll
+            for (int p = 3; p >= 0; --p) {
+                const f2v s = q[p] - th;
+                inv = (inv << 1) | (__float_as_uint(s.y) >> 31);
+                inv = (inv << 1) | (__float_as_uint(s.x) >> 31);
+            }
+            const uint32_t mask = ~inv & 0xffu;
+            my[min(cnt, (uint32_t)kCand) * kRB] = (8u * b) | (mask << 24);
+            cnt += mask != 0u ? 1u : 0u;
+        }
+    }
+    return cnt;
+}
+
+// hit_world with the prefiltered scan: same (best, idx) as the in-order
+// reference scan (candidates are resolved with the reference's ops; any
+// overflowing list or non-finite root takes hit_blocks_seq).
+__device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
+                                             float t_min, float &best, uint32_t *list) {
+    const cfloat_p soa = (cfloat_p)S.soa;
+    const uint32_t nblk = S.n_pad / 8;
+    const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    const float best0 = best;
+    int idx = -1;
+    const uint32_t cnt = scan_prefilter((cfloat_p)S.pre, nblk, T, list);
+    if (!resolve_candidates<24>(soa, 0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
+        RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
+        best = best0;
+        idx = hit_blocks_seq(soa, nblk, 0, o, d, a, inv_a, t_min, best, -1);
+    }
+    return idx;
+}
+#endif
+
+// One ray segment against the whole scene with sphere data read through
+// scalar loads (RTX_SRC 1 and the debug kernel).
+__device__ __forceinline__ int trace_scalar(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
+                                            float &best, uint32_t *list) {
+#if RTX_PREFILTER
+    return hit_world_pre(S, o, d, a, inv_a, t_min, best, list);
+#else
+    return hit_world((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1, list);
 #endif
 }
 
@@ -652,16 +744,14 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     // dynamic LDS: [candidate list, kListBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    const uint32_t nblk = P.scene.n_pad / 8;
     const int last = (int)P.scene.n - 1;
 #if RTX_SRC == 0
+    const uint32_t nblk = P.scene.n_pad / 8;
     float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kRB) s_blk4[i] = g4[i];
     __syncthreads();
-#else
-    const cfloat_p soa = (cfloat_p)P.scene.soa;
 #endif
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
@@ -727,7 +817,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
-                    my_hit = hit_world(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, my_best, -1, list);
+                    my_hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
                 shade(P, F, L, min(my_hit, last), my_best);
             }
@@ -740,7 +830,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #if RTX_SRC == 0
             const int hit = hit_world(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
 #else
-            const int hit = hit_world(soa, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
+            const int hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
 #endif
             RTX_PROF(1)
             shade(P, F, L, min(hit, last), best);
@@ -909,8 +999,7 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx = min(hit_world((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1, list),
-                        (int)S.n - 1);
+    const int idx = min(trace_scalar(S, o, d, a, inv_a, t_min, best, list), (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
         for (int k = 0; k < 10; ++k) r[k] = 0.0f;

@@ -1,0 +1,110 @@
+// rtx_prefilter.h — the conservative line-distance prefilter of hit_world's
+// scan (DESIGN.md §3 "prefilter"), shared by the HIP kernel and the CPU
+// margin checker (tests/prefilter_check.cpp).
+//
+// The reference rejects sphere i when disc = hb^2 - a*cc < 0
+// (ShaderCompute.hlsl:163-166 / Sphere.cpp:11-13). In exact arithmetic
+// disc / a = r^2 - dperp^2, dperp = distance from the sphere centre to the
+// ray's LINE. The kernel's scan does not evaluate the reference's disc
+// (11 fp32 ops per sphere); it evaluates
+//     Q = R_i - (c.u - o.u)^2 - (c.v - o.v)^2          (7 fp32 ops)
+// with (u, v) an orthonormal basis of the plane perpendicular to d, u
+// chosen with u.y = 0 so that c.u needs two fma instead of three, and flags
+// the sphere as a candidate when Q >= thr. R_i = r^2 + margin(c, r) and
+// thr = -margin(o) are inflated so that
+//     reference disc >= 0 (or NaN)  ==>  Q >= thr,
+// i.e. the prefilter never drops a sphere the reference would test further.
+// A flagged sphere is resolved with the reference's own op sequence
+// (rtx_kernels.hip, resolve_candidates), which rejects false positives, so
+// the scan's answer is bit-identical to the reference's.
+//
+// Error bound (u = unit roundoff 2^-24, S = |c| + |o|):
+//   reference disc rounding, divided by a:    13|oc|^2 + 7r^2
+//   oc = fl(o - c) perturbation:               2|oc|^2
+//   basis (u, v) error (<= 4u, 9u per vector): 20|oc|^2
+//   c.u - o.u, c.v - o.v chains (4u S, 6u S):  15 S^2
+//   final two fma:                              4r^2
+//   total <= u (50 S^2 + 11 r^2) <= u (100|c|^2 + 100|o|^2 + 11 r^2)
+// The margins below are 1.6e-5 (= 268u) per |c|^2 and |o|^2 and 2e-6
+// (= 33u) per r^2, i.e. >= 2.6x that bound, plus an absolute 1e-24 that
+// covers subnormal rounding in the region the per-lane `safe` test admits
+// (a in [2^-40, 2^40], ray not within ~2^-20 rad of vertical, no fp32
+// overflow). Lanes outside that region get u = v = 0 and thr = -inf: every
+// sphere is flagged and the lane ends on the exact sequential path.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RTX_HD __host__ __device__ __forceinline__
+#else
+#define RTX_HD static inline
+#endif
+
+namespace rtx {
+
+constexpr float kPreMarginO = 1.6e-5f;  // per |o|^2 (ray side, thr)
+constexpr double kPreMarginC = 1.6e-5;  // per |c|^2 (sphere side, R_i)
+constexpr double kPreMarginR = 2e-6;    // per r^2   (sphere side, R_i)
+constexpr float kPreFloor = 1e-24f;
+
+struct LineTest {
+    float ux, uz;      // u = (-dz, 0, dx) / |(dx, dz)|
+    float vx, vy, vz;  // v = d/|d| x u
+    float nou, nov;    // -(o.u), -(o.v)
+    float thr;         // flag the sphere when Q >= thr
+};
+
+// Sphere side, at upload, in double, rounded UP to fp32. r2 is the
+// reference's fl(r*r) (the value the exact scan negates into its soa).
+inline float prefilter_R(float cx, float cy, float cz, float r2) {
+    const double c2 = (double)cx * cx + (double)cy * cy + (double)cz * cz;
+    const double R = (double)r2 + kPreMarginC * c2 + kPreMarginR * (double)r2 + (double)kPreFloor;
+    float f = (float)R;
+    if ((double)f < R) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// Ray side, once per segment. `a` is the reference's |d|^2 (fma form),
+// `smag` an upper bound of |c| + r over the scene (rtx_upload_world).
+RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy, float dz, float a,
+                                float smag) {
+    LineTest T;
+    const float n2 = fmaf(dx, dx, dz * dz);
+    const float o2 = fmaf(ox, ox, fmaf(oy, oy, oz * oz));
+    // a in [2^-40, 2^40]; d not within ~2^-20 rad of the y axis; S = smag +
+    // |o| with S^2 and a*S^2 <= 1e36 (no fp32 overflow in disc or Q).
+    // NaN or infinite inputs fail these tests.
+    const float so = smag + sqrtf(o2);
+    const float so2 = so * so;
+    const bool safe = a >= 9.094947e-13f && a <= 1.0995116e12f && n2 >= a * 9.094947e-13f &&
+                      so2 <= 1e36f && a * so2 <= 1e36f;
+    if (!safe) {
+        T.ux = T.uz = T.vx = T.vy = T.vz = T.nou = T.nov = 0.0f;
+        T.thr = -INFINITY;
+        return T;
+    }
+    const float sn = sqrtf(n2);
+    const float inv_n = 1.0f / sn;
+    T.ux = -dz * inv_n;
+    T.uz = dx * inv_n;
+    const float w = 1.0f / (sqrtf(a) * sn);
+    T.vx = (dx * dy) * w;
+    T.vy = -(n2 * w);
+    T.vz = (dy * dz) * w;
+    T.nou = -fmaf(oz, T.uz, ox * T.ux);
+    T.nov = -fmaf(oz, T.vz, fmaf(oy, T.vy, ox * T.vx));
+    T.thr = -fmaf(o2, kPreMarginO, kPreFloor);
+    return T;
+}
+
+// Q for one sphere; the kernel runs the same op sequence on sphere pairs
+// (v_pk_fma_f32), i.e. the same IEEE fma per element.
+RTX_HD float line_test_q(const LineTest &T, float cx, float cy, float cz, float R) {
+    const float pu = fmaf(cx, T.ux, fmaf(cz, T.uz, T.nou));
+    const float pv = fmaf(cx, T.vx, fmaf(cy, T.vy, fmaf(cz, T.vz, T.nov)));
+    return fmaf(-pv, pv, fmaf(-pu, pu, R));
+}
+
+}  // namespace rtx

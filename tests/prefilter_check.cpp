@@ -1,0 +1,117 @@
+// prefilter_check.cpp — CPU check of the exactness claim of the scan's
+// prefilter (raytrace-we-gpu_amd/csrc/rtx_prefilter.h): over many
+// adversarial ray/sphere pairs — near-tangent lines (relative distance
+// 1e-9 .. 1e-1 from the silhouette), tiny and huge directions, near-vertical
+// rays, far origins, centre magnitudes 1e-2 .. 1e4, radii 1e-3 .. 1e3 —
+// whenever the reference's fp32 discriminant is >= 0 or NaN
+// (ShaderCompute.hlsl:158-166; the op order of oracle/rtx_oracle.c
+// hit_world32), the prefilter must flag the sphere.
+// Prints one JSON line; exit status 1 if any reference candidate is missed.
+// Build: g++ -O2 -std=c++17 -ffp-contract=off -mfma prefilter_check.cpp
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../raytrace-we-gpu_amd/csrc/rtx_prefilter.h"
+
+static unsigned long long g_s = 0x9e3779b97f4a7c15ull;
+static double uni() {
+    g_s ^= g_s << 13;
+    g_s ^= g_s >> 7;
+    g_s ^= g_s << 17;
+    return (double)(g_s >> 11) * (1.0 / 9007199254740992.0);
+}
+static double sym() { return 2.0 * uni() - 1.0; }
+static void unit(double v[3]) {
+    do {
+        v[0] = sym(), v[1] = sym(), v[2] = sym();
+    } while (v[0] * v[0] + v[1] * v[1] + v[2] * v[2] < 1e-6);
+    const double n = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    v[0] /= n, v[1] /= n, v[2] /= n;
+}
+
+// hit_world32's discriminant (oracle/rtx_oracle.c), reference op order.
+static float ref_disc(const float o[3], const float d[3], const float c[3], float negr2, float a) {
+    const float ocx = o[0] - c[0], ocy = o[1] - c[1], ocz = o[2] - c[2];
+    const float hb = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
+    const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, negr2)));
+    return fmaf(hb, hb, -(a * cc));
+}
+
+int main(int argc, char **argv) {
+    const long n = argc > 1 ? std::atol(argv[1]) : 2000000;
+    long ref_pos = 0, flagged = 0, missed = 0, unsafe = 0, false_pos = 0;
+    double max_used = -1e300;
+    for (long k = 0; k < n; ++k) {
+        double cd[3], dir[3], e[3];
+        unit(cd);
+        const double cs = std::pow(10.0, -2.0 + 6.0 * uni());
+        const double r = std::pow(10.0, -3.0 + 6.0 * uni());
+        unit(dir);
+        const double pv = uni();
+        if (pv < 0.05) {  // near-vertical
+            const double eps = std::pow(10.0, -8.0 + 6.0 * uni());
+            dir[0] = eps * sym(), dir[2] = eps * sym(), dir[1] = uni() < 0.5 ? -1.0 : 1.0;
+        } else if (pv < 0.08) {  // axis-aligned
+            const int ax = (int)(uni() * 3.0) % 3;
+            dir[0] = dir[1] = dir[2] = 0.0;
+            dir[ax] = uni() < 0.5 ? -1.0 : 1.0;
+        }
+        // e: unit vector perpendicular to dir
+        double t[3];
+        unit(t);
+        const double td = t[0] * dir[0] + t[1] * dir[1] + t[2] * dir[2];
+        const double dn = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+        for (int i = 0; i < 3; ++i) e[i] = t[i] - td / dn * dir[i];
+        const double en = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        if (en < 1e-9) continue;
+        for (int i = 0; i < 3; ++i) e[i] /= en;
+        // line at distance r (1 + delta) from the centre (delta from 1e-9 to 0.1, either side),
+        // or anywhere inside 3r for a fifth of the cases
+        double dist;
+        if (uni() < 0.8) {
+            const double delta = std::pow(10.0, -9.0 + 8.0 * uni()) * (uni() < 0.5 ? -1.0 : 1.0);
+            dist = r * (1.0 + delta);
+        } else {
+            dist = 3.0 * r * uni();
+        }
+        const double along = sym() * std::pow(10.0, -1.0 + 4.0 * uni()) * std::fmax(r, 1.0);
+        const double dlen = std::pow(10.0, -3.0 + 6.0 * uni());
+        float c[3], o[3], d[3];
+        for (int i = 0; i < 3; ++i) {
+            c[i] = (float)(cs * cd[i]);
+            o[i] = (float)(cs * cd[i] + dist * e[i] - along * dir[i]);
+            d[i] = (float)(dlen * dir[i]);
+        }
+        const float rf = (float)r;
+        const float r2 = rf * rf;
+        const float a = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
+        const double sm = std::sqrt((double)c[0] * c[0] + (double)c[1] * c[1] + (double)c[2] * c[2]) + rf;
+        float smag = (float)sm;
+        if ((double)smag < sm) smag = std::nextafter(smag, INFINITY);
+        const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
+        const float R = rtx::prefilter_R(c[0], c[1], c[2], r2);
+        const float q = rtx::line_test_q(T, c[0], c[1], c[2], R);
+        const float disc = ref_disc(o, d, c, -r2, a);
+        const bool ref = !(disc < 0.0f);
+        const bool flag = !(q < T.thr);
+        ref_pos += ref;
+        flagged += flag;
+        false_pos += flag && !ref;
+        if (T.thr == -INFINITY) ++unsafe;
+        if (ref && !flag) {
+            if (++missed <= 5)
+                std::fprintf(stderr, "MISS c=(%.9g %.9g %.9g) r=%.9g o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) disc=%.9g q=%.9g thr=%.9g\n",
+                             c[0], c[1], c[2], rf, o[0], o[1], o[2], d[0], d[1], d[2], disc, q, T.thr);
+        }
+        if (ref && T.thr != -INFINITY) {
+            // share of the margin the rounding errors used: (estimated dperp^2 - r^2) / (R - thr - r^2)
+            const double used = (((double)R - q) - r2) / ((double)R - T.thr - r2);
+            if (used > max_used) max_used = used;
+        }
+    }
+    std::printf("{\"cases\": %ld, \"reference_candidates\": %ld, \"flagged\": %ld, \"false_positives\": %ld, "
+                "\"unsafe_lanes\": %ld, \"missed\": %ld, \"max_margin_used\": %.6g}\n",
+                n, ref_pos, flagged, false_pos, unsafe, missed, max_used);
+    return missed ? 1 : 0;
+}

@@ -121,6 +121,37 @@ def test_hit_world_ties_and_padding(gpu_ctx, oracle, rtx):
             assert not np.any(np.isin(want[hit0, 9], [0])), "tie must go to the later duplicate"
 
 
+def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx):
+    """Rays whose line passes within 1e-9..1e-2 (relative) of a sphere's
+    silhouette, on either side, plus near-vertical rays (the prefilter's
+    degenerate basis), tiny and huge direction lengths and origins far down
+    the line: the kernel's prefiltered scan (rtx_prefilter.h) must return the
+    reference scan's records bit for bit."""
+    rng = np.random.default_rng(11)
+    world = rtx.random_world(11, depth=1, spp=1)
+    sph = world.spheres.astype(np.float64)
+    n = 30000
+    pick = rng.integers(0, len(sph), n)
+    c, r = sph[pick, :3], sph[pick, 3]
+    dirs = rng.normal(size=(n, 3))
+    vert = rng.random(n) < 0.08
+    dirs[vert] = np.stack([rng.normal(scale=1e-7, size=vert.sum()), np.sign(rng.normal(size=vert.sum())),
+                           rng.normal(scale=1e-7, size=vert.sum())], 1)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    e = np.cross(dirs, rng.normal(size=(n, 3)))
+    e /= np.linalg.norm(e, axis=1, keepdims=True)
+    delta = np.sign(rng.normal(size=n)) * 10.0 ** rng.uniform(-9, -2, n)
+    p = c + (r * (1 + delta))[:, None] * e
+    o = p - rng.uniform(-40, 40, n)[:, None] * dirs
+    d = dirs * (10.0 ** rng.uniform(-3, 3, n))[:, None]
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    gpu_ctx.upload_world(world)
+    got = gpu_ctx.debug_hit_world(rays)
+    want = oracle.hit_world_f32(world, rays)
+    assert_bits_equal(got, want, "grazing rays")
+    assert (want[:, 0] == 1).mean() > 0.3
+
+
 # ---------------------------------------------------------------------------
 # whole-frame parity
 # ---------------------------------------------------------------------------

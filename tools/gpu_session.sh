@@ -26,19 +26,19 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     ubench) run ubench 120 ./tools/ubench_valu ;;
-    tests)  run tests 900 python -m pytest tests -m gpu -q -rA ;;
+    tests)  run tests 900 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                 python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
     c3b)    run c3b 900 python bench.py --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 --pmc off ;;
     c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --pmc off ;;
-    variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ;;
+    variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ${VNAMES:-} ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
     timeline) run timeline 300 python tools/wave_timeline.py ;;
     vtimeline) for v in ${VTL:-blk64 lpt lpt_blk64}; do
               run timeline_$v 300 python tools/wave_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_$v.so; done ;;
-    sprof)  run sprof 300 python tools/section_prof.py raytrace-we-gpu_amd/lib/variants/librtx_prof.so raytrace-we-gpu_amd/lib/variants/librtx_prof_merge.so ;;
+    sprof)  run sprof 300 python tools/section_prof.py raytrace-we-gpu_amd/lib/variants/librtx_prof.so raytrace-we-gpu_amd/lib/variants/librtx_pre0_prof.so ;;
     cost)   run cost 600 python tools/cost_analysis.py --out "$OUT/cost.npz" ;;
     c5)     run c5 900 python tools/variant_bench.py --rounds 2 --frames 1 --spp 16 --grid 159 --max-spheres 100000 ${C5V:-} ;;
     diag)   run diag 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
