@@ -45,33 +45,13 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best pre0 prof pre0_prof
-VFLAGS_pre0          := -DRTX_PREFILTER=0
-VFLAGS_pre0_prof     := -DRTX_PREFILTER=0 -DRTX_DIAG_PROF=1
-VFLAGS_best          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8
-VFLAGS_blk64         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=0 -DRTX_BLOCK=64
-VFLAGS_blk128        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=128
-VFLAGS_blk64_w7      := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_BLOCK=64 -DRTX_WAVES_PER_SIMD=7
-VFLAGS_lpt           := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1
-VFLAGS_lpt_blk64     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_BLOCK=64
-VFLAGS_lpt_r0        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_RADIUS=0
-VFLAGS_lpt_r2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_RADIUS=2
-VFLAGS_lpt_s2        := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2
-VFLAGS_lpt_cw4       := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_CW=4
-VFLAGS_lpt_s2_cw4    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_SPP=2 -DRTX_LPT_CW=4
-VFLAGS_lpt_b1k       := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024
-VFLAGS_lpt_b1k_r2    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_RADIUS=2
-VFLAGS_lpt_b1k_cw4   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_CW=4
-VFLAGS_lpt_b1k_s2    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_LPT_BUCKETS=1024 -DRTX_LPT_SPP=2
-VFLAGS_lpt_coop4     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=4
-VFLAGS_lpt_coop8     := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8
-VFLAGS_lpt_coop16    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=16
-VFLAGS_blk64_coop8   := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=0 -DRTX_BLOCK=64 -DRTX_COOP_MAX=8
-VFLAGS_merge         := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_SHADE_MERGE=1
-VFLAGS_prof          := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_DIAG_PROF=1
-VFLAGS_prof_merge    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_COOP_MAX=8 -DRTX_DIAG_PROF=1 -DRTX_SHADE_MERGE=1
-VFLAGS_lpt_blk128    := -DRTX_DEFER=1 -DRTX_SRC=1 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1 -DRTX_PERSISTENT=1 -DRTX_BLOCK=128
-VFLAGS_lds_stream_b8 := -DRTX_DEFER=1 -DRTX_SRC=0 -DRTX_BATCH=8 -DRTX_LISTMASK=1 -DRTX_ANYMAX=1
+VARIANTS := best prof t1r10a3 t1r10a2 t1r10a3m2 r10
+VFLAGS_best          :=
+VFLAGS_prof          := -DRTX_DIAG_PROF=1
+VFLAGS_t1r10a3       := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=3.0 -DRTX_HEAVY1_ALPHA=3.0
+VFLAGS_t1r10a2       := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=2.0 -DRTX_HEAVY1_ALPHA=2.0
+VFLAGS_t1r10a3m2     := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=3.0 -DRTX_HEAVY1_ALPHA=3.0 -DRTX_HEAVY1_WAVE=2
+VFLAGS_r10           := -DRTX_HEAVY_RHO=10.0
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

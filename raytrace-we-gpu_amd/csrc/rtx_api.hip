@@ -51,6 +51,7 @@ struct rtx_ctx {
     // scene (device)
     float *d_soa = nullptr;
     float *d_pre = nullptr;  // prefilter blocks (rtx_prefilter.h)
+    float4 *d_pre4 = nullptr;  // prefilter data per sphere (tail coop)
     float smag = 0.0f;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
@@ -90,11 +91,13 @@ int set_device(rtx_ctx *c) {
 void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_soa);
     (void)hipFree(c->d_pre);
+    (void)hipFree(c->d_pre4);
     (void)hipFree(c->d_cen);
     (void)hipFree(c->d_mtype);
     (void)hipFree(c->d_mval);
     c->d_soa = nullptr;
     c->d_pre = nullptr;
+    c->d_pre4 = nullptr;
     c->d_cen = nullptr;
     c->d_mtype = nullptr;
     c->d_mval = nullptr;
@@ -105,6 +108,7 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     rtx::KScene s;
     s.soa = c->d_soa;
     s.pre = c->d_pre;
+    s.pre4 = c->d_pre4;
     s.smag = c->smag;
     s.cen = c->d_cen;
     s.mtype = c->d_mtype;
@@ -217,7 +221,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     const uint32_t n_pad = (n + rtx::kPad - 1) / rtx::kPad * rtx::kPad;
     std::vector<float> soa(4 * (size_t)n_pad), pre(4 * (size_t)n_pad);
     double smag = 0.0;  // max |c| + |r|, for the prefilter's overflow guard
-    std::vector<float4> cen(n), mval(n);
+    std::vector<float4> cen(n), mval(n), pre4(n);
     std::vector<int> mtype(n);
     for (uint32_t i = 0; i < n_pad; ++i) {
         // padding: copies of sphere n-1 (see rtx::KScene)
@@ -236,6 +240,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         pb[24 + i % 8] = rtx::prefilter_R(blk[i % 8], blk[8 + i % 8], blk[16 + i % 8], r2);
         const double cx = blk[i % 8], cy = blk[8 + i % 8], cz = blk[16 + i % 8];
         smag = std::max(smag, std::sqrt(cx * cx + cy * cy + cz * cz) + std::fabs((double)r));
+        if (i < n) pre4[i] = make_float4(pb[i % 8], pb[8 + i % 8], pb[16 + i % 8], pb[24 + i % 8]);
     }
     float smag_f = (float)smag;
     if ((double)smag_f < smag) smag_f = std::nextafter(smag_f, INFINITY);
@@ -254,6 +259,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     const size_t cap = n ? n : 1;
     RTX_HIP(hipMalloc(&c->d_soa, (n_pad ? 4 * (size_t)n_pad : 4) * sizeof(float)));
     RTX_HIP(hipMalloc(&c->d_pre, (n_pad ? 4 * (size_t)n_pad : 4) * sizeof(float)));
+    RTX_HIP(hipMalloc(&c->d_pre4, cap * sizeof(float4)));
     RTX_HIP(hipMalloc(&c->d_cen, cap * sizeof(float4)));
     RTX_HIP(hipMalloc(&c->d_mtype, cap * sizeof(int)));
     RTX_HIP(hipMalloc(&c->d_mval, cap * sizeof(float4)));
@@ -262,6 +268,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (n) {
         RTX_HIP(hipMemcpyAsync(c->d_soa, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_pre, pre.data(), pre.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_pre4, pre4.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cen, cen.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -409,7 +416,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         (void)hipFree(c->d_sched);
         c->d_sched = nullptr;
         c->sched_pixels = 0;
-        RTX_HIP(hipMalloc(&c->d_sched, (2 * npix + 2 * rtx::kCostBuckets) * sizeof(uint32_t)));
+        RTX_HIP(hipMalloc(&c->d_sched, (2 * npix + 2 * rtx::kCostBuckets + 4) * sizeof(uint32_t)));
         c->sched_pixels = npix;
     }
     rtx::KSchedule sched;

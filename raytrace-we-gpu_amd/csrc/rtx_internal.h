@@ -25,6 +25,7 @@ namespace rtx {
 struct KScene {
     const float *soa;
     const float *pre;
+    const float4 *pre4;  // [n] (cx, cy, cz, R): the prefilter data per sphere (tail coop)
     const float4 *cen;
     const int *mtype;
     const float4 *mval;
@@ -52,6 +53,8 @@ struct KParams {
     unsigned long long *wave_times;  // diagnostic: per-wave (start, end) s_memrealtime, or NULL
     const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
+    uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
+    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
 };
 
 // Longest-processing-time-first scheduling for the persistent kernel: a
@@ -62,7 +65,7 @@ struct KParams {
 struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
-    uint32_t *buckets;  // [2 * nbuckets]: counts, cursors (zeroed per launch)
+    uint32_t *buckets;  // [2 * nbuckets + 4]: counts, cursors, heavy counters and ends (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
 };

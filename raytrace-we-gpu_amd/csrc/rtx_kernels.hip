@@ -107,6 +107,30 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_PREFILTER  // 1: scan with the line-distance prefilter (rtx_prefilter.h; RTX_SRC 1 only)
 #define RTX_PREFILTER 1
 #endif
+#ifndef RTX_HEAVY_WAVE  // heavy pixels per group-coop wave (0: no heavy split)
+#define RTX_HEAVY_WAVE 8
+#endif
+#ifndef RTX_HEAVY_ALPHA  // heavy iff key > alpha * (a lane's share of the summed keys)
+#define RTX_HEAVY_ALPHA 2.0
+#endif
+#ifndef RTX_PRIO_FRAC_X100  // hot-wave priority: prio_slots = this % of the resident lanes (0 = off)
+#define RTX_PRIO_FRAC_X100 20
+#endif
+#ifndef RTX_TAIL_PRIO  // wave priority of a normal wave in its coop tail
+#define RTX_TAIL_PRIO 1
+#endif
+#ifndef RTX_HEAVY_RHO  // "small" frame share: fewer pixels than rho * resident lanes
+#define RTX_HEAVY_RHO 1.2
+#endif
+#ifndef RTX_HEAVY1_ALPHA  // tier 1 iff key > alpha1 * a lane's share of the summed keys
+#define RTX_HEAVY1_ALPHA 2.0
+#endif
+#ifndef RTX_HEAVY1_ALPHA_SMALL  // the same for a small frame share
+#define RTX_HEAVY1_ALPHA_SMALL 4.0
+#endif
+#ifndef RTX_HEAVY1_WAVE  // tier-1 heavy pixels per wave
+#define RTX_HEAVY1_WAVE 1
+#endif
 #ifndef RTX_BLOCK  // threads per render workgroup (64 = one wave: freed slots refill independently)
 #define RTX_BLOCK 256
 #endif
@@ -391,23 +415,24 @@ __device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, 
 #endif
 }
 
-#if RTX_PREFILTER
 // ---- prefiltered scan (rtx_prefilter.h) -----------------------------------
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Q = R - pu^2 - pv^2 for sphere pairs (v_pk_fma_f32), 8 spheres per step
-// from the `pre` blocks; one max + ballot skips a step in which no lane's
-// line comes near any of the 8. A lane with flagged spheres appends ONE
-// entry per 8-sphere block: local index of the block's first sphere |
-// 8-bit mask << 24 (so n_pad <= 2^24, checked at upload).
-__device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t nblk, const LineTest &T,
-                                                   uint32_t *list) {
-    uint32_t cnt = 0;
+// from the `pre` blocks, starting at block b; one max + ballot skips a step
+// in which no lane's line comes near any of the 8. A lane with flagged
+// spheres appends ONE entry per 8-sphere block: local index of the block's
+// first sphere | 8-bit mask << 24 (so n_pad <= 2^24, checked at upload).
+// Returns the block to resume at: nblk, or earlier once some lane's list is
+// full (kCand entries) and must be resolved first (wave-uniform).
+__device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk,
+                                                   const LineTest &T, uint32_t *list, uint32_t &cnt) {
+    cnt = 0;
     uint32_t *my = list + threadIdx.x;
     const f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
     const f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
-    for (uint32_t b = 0; b < nblk; ++b) {
+    for (; b < nblk; ++b) {
         const cfloat_p blk = pre + 32 * b;
         f2v q[4];
 #pragma unroll
@@ -420,8 +445,9 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t nblk, 
             const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
             q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
         }
-        const float mx = fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), fmaxf(q[1].x, q[1].y)),
-                               fmaxf(fmaxf(q[2].x, q[2].y), fmaxf(q[3].x, q[3].y)));
+        // a chain, so that it folds into v_max3_f32
+        const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
+                                                 q[2].y), q[3].x), q[3].y);
         RTX_DIAG_ADD(0, 1u);
         if (__ballot(!(mx < T.thr)) != 0ull) {
             RTX_DIAG_ADD(1, 1u);
@@ -436,32 +462,88 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t nblk, 
                 inv = (inv << 1) | (__float_as_uint(s.x) >> 31);
             }
             const uint32_t mask = ~inv & 0xffu;
-            my[min(cnt, (uint32_t)kCand) * kRB] = (8u * b) | (mask << 24);
+            my[cnt * kRB] = (8u * b) | (mask << 24);  // cnt < kCand here
             cnt += mask != 0u ? 1u : 0u;
+            if (__ballot(cnt == (uint32_t)kCand) != 0ull) return b + 1;
         }
     }
-    return cnt;
+    return nblk;
+}
+
+// Resolve the lane's list (m entries: first sphere index | mask << 24)
+// with the reference's own ops (Sphere.cpp:6-24 / ShaderCompute.hlsl:
+// 155-186), one candidate per lane per iteration, no branch inside an
+// iteration. Sphere data: cen[i] = (center, radius) in one load; -(r*r) is
+// the same fp32 product the upload negates into soa; a padded index (>= n)
+// reads sphere n-1, whose copy it is. A prefilter false positive (exact
+// disc < 0) is skipped, like the reference's `if (d < 0) return false`.
+// Returns false if a candidate has a non-finite root (the lane then takes
+// hit_blocks_seq).
+__device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint32_t n, const uint32_t *list,
+                                            uint32_t m, f3 o, f3 d, float a, float inv_a, float t_min,
+                                            float &best, int &idx) {
+    const float inf = __uint_as_float(0x7f800000u);
+    bool ok = true;
+    uint32_t j = 0;
+    uint32_t e = list[threadIdx.x];  // entry 0 (unused when m == 0)
+    RTX_DIAG_ADD(4, (uint32_t)__popcll(__ballot(m != 0u)));
+    while (__ballot(j < m) != 0ull) {
+        RTX_DIAG_ADD(2, 1u);
+        const bool live = j < m;
+        const uint32_t i = (e & 0xffffffu) + (uint32_t)__builtin_ctz(live ? (e >> 24) : 1u);
+        e &= e - (1u << 24);  // drop that candidate from the mask
+        const bool adv = live && (e >> 24) == 0u;
+        j += adv ? 1u : 0u;
+        const uint32_t nx = list[min(j, (uint32_t)kCand) * kRB + threadIdx.x];
+        e = adv ? nx : e;
+        const float4 sc = cen[min(i, n - 1u)];
+        const float ocx = o.x - sc.x;
+        const float ocy = o.y - sc.y;
+        const float ocz = o.z - sc.z;
+        const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(sc.w * sc.w))));
+        const float disc = fmaf(hb, hb, -(a * cc));
+        const bool cand = live && !(disc < 0.0f);
+        const float sq = sqrtf(disc);
+        const float rn = (-hb - sq) * inv_a;
+        const float rf = (-hb + sq) * inv_a;
+        ok = ok && !(cand && !(fabsf(rn) < inf && fabsf(rf) < inf));
+        const bool use_n = !(rn < t_min);
+        const float c = use_n ? rn : rf;
+        const int g = (int)i;
+        const bool acc = cand && (use_n || !(rf < t_min)) && (c < best || (c == best && g > idx));
+        best = acc ? c : best;
+        idx = acc ? g : idx;
+    }
+    return ok;
 }
 
 // hit_world with the prefiltered scan: same (best, idx) as the in-order
-// reference scan (candidates are resolved with the reference's ops; any
-// overflowing list or non-finite root takes hit_blocks_seq).
+// reference scan. Candidates are resolved in rounds (a round ends when some
+// lane's list is full); the (min c, largest index) rule is
+// order-independent, so rounds compose. A non-finite root takes
+// hit_blocks_seq.
 __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
                                              float t_min, float &best, uint32_t *list) {
-    const cfloat_p soa = (cfloat_p)S.soa;
+    const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const float best0 = best;
     int idx = -1;
-    const uint32_t cnt = scan_prefilter((cfloat_p)S.pre, nblk, T, list);
-    if (!resolve_candidates<24>(soa, 0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
+    bool ok = true;
+    uint32_t b = 0;
+    do {
+        uint32_t cnt;
+        b = scan_prefilter(pre, b, nblk, T, list, cnt);
+        ok = resolve_pre(S.cen, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx) && ok;
+    } while (b < nblk);
+    if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
-        idx = hit_blocks_seq(soa, nblk, 0, o, d, a, inv_a, t_min, best, -1);
+        idx = hit_blocks_seq((cfloat_p)S.soa, nblk, 0, o, d, a, inv_a, t_min, best, -1);
     }
     return idx;
 }
-#endif
 
 // One ray segment against the whole scene with sphere data read through
 // scalar loads (RTX_SRC 1 and the debug kernel).
@@ -474,62 +556,116 @@ __device__ __forceinline__ int trace_scalar(const KScene &S, f3 o, f3 d, float a
 #endif
 }
 
-// ---- wave-cooperative hit_world (frame tail) ------------------------------
-__device__ __forceinline__ float read_lane(float v, int src) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
-}
+// ---- group-cooperative hit_world (frame tail) ------------------------------
+// Once the pixel queue is empty a wave runs on until its last pixel ends,
+// and the frame ends on the most expensive pixels. With m <= RTX_COOP_MAX
+// rays left, the wave traces them together: ray r (the r-th active lane)
+// by the g = 64 / 2^ceil(log2 m) lanes [r*g, r*g + g). Lane k of a group
+// runs the prefilter over spheres k, k+g, ... (pre4), resolves what it
+// flagged with the reference's ops (resolve_pre), and the group reduces
+// (min c, largest index): the order-independent rule of the deferred
+// resolution, hence the in-order scan's answer. The ray's own lane reads the
+// result back through LDS. A non-finite root in the group sends the ray to
+// the exact sequential path (`seq`).
+constexpr uint32_t kCoopSlots = 32;                                   // rays per wave in coop mode
+constexpr uint32_t kCoopWaveBytes = kCoopSlots * 10 * sizeof(float);  // ray (8 floats) + 64-bit key
+constexpr uint32_t kCoopBytes = (kRB / 64) * kCoopWaveBytes;
+#ifndef RTX_COOP_STEP
+#define RTX_COOP_STEP 2
+#endif
+constexpr uint32_t kCoopStep = RTX_COOP_STEP;  // spheres per coop step (reads in flight)
+constexpr uint32_t kCoopLds = 768;  // scenes up to this many spheres keep pre4 in LDS for the coop (12 KiB)
+static_assert(RTX_COOP_MAX <= (int)kCoopSlots, "RTX_COOP_MAX must be <= 32");
 
-// ONE wave-uniform ray against all n spheres: lane l takes spheres l, l+64,
-// ... with the arithmetic of resolve_candidates, keeps its own (min c,
-// largest index) and the wave reduces the 64 results — the same
-// order-independent rule, hence the in-order scan's answer (see above).
-// Any non-finite root sets `seq`: the caller redoes the ray with hit_world.
-__device__ __forceinline__ int hit_world_coop(const float *soa, uint32_t n, f3 o, f3 d, float a,
-                                              float inv_a, float t_min, float &best, bool &seq) {
-    const float inf = __uint_as_float(0x7f800000u);
-    float bc = inf;
-    int bg = -1;
-    bool bad = false;
-#pragma unroll 2
-    for (uint32_t i = threadIdx.x & 63u; i < n; i += 64u) {
-        const float *blk = soa + 32 * (i >> 3);
-        const uint32_t q = i & 7u;
-        const float ocx = o.x - blk[q];
-        const float ocy = o.y - blk[8 + q];
-        const float ocz = o.z - blk[16 + q];
-        const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + q])));
-        const float disc = fmaf(hb, hb, -(a * cc));
-        if (!(disc < 0.0f)) {
-            const float sq = sqrtf(disc);
-            const float rn = (-hb - sq) * inv_a;
-            const float rf = (-hb + sq) * inv_a;
-            if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) bad = true;
-            const bool use_n = !(rn < t_min);
-            const float c = use_n ? rn : rf;
-            if ((use_n || !(rf < t_min)) && (c < bc || (c == bc && (int)i > bg))) {
-                bc = c;
-                bg = (int)i;
-            }
-        }
+template <typename Q4>
+__device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64_t act, bool active, f3 o,
+                                                f3 d, float a, float inv_a, float t_min, float *ws,
+                                                uint32_t *list, float &best, bool &seq) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m = (uint32_t)__popcll(act);
+    const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
+    const uint32_t g = 1u << lg;
+    const uint32_t rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    uint32_t *keys = reinterpret_cast<uint32_t *>(ws + 8 * kCoopSlots);
+    if (active) {
+        float *w = ws + 8 * rank;
+        w[0] = o.x;
+        w[1] = o.y;
+        w[2] = o.z;
+        w[3] = d.x;
+        w[4] = d.y;
+        w[5] = d.z;
+        w[6] = a;
+        w[7] = inv_a;
     }
-    seq = __ballot(bad) != 0ull;
-    if (seq) return -1;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t r = lane >> lg, k = lane & (g - 1u);
+    const bool valid = r < m;
+    const float *w = ws + 8 * (valid ? r : 0u);  // the group's ray (re-read where needed: fewer live VGPRs)
+    const LineTest T = line_test_setup(w[0], w[1], w[2], w[3], w[4], w[5], w[6], S.smag);
+    const uint32_t n = S.n;
+    // lane k of a group scans the contiguous chunk [k*ch, k*ch + ch) of the
+    // spheres (ch odd, so the group's LDS reads fall in different banks),
+    // kCoopStep spheres per step with all their reads issued before the tests
+    const uint32_t ch = ((n + g - 1u) >> lg) | 1u;
+    const uint32_t i1 = valid ? min((k + 1u) * ch, n) : 0u;
+    uint32_t i = valid ? min(k * ch, n) : 0u;
+    uint32_t *my = list + threadIdx.x;
+    float bc = __uint_as_float(0x7f800000u);
+    int bg = -1;
+    bool ok = true;
+    do {
+        uint32_t cnt = 0;
+        for (;;) {
+            const bool more = i < i1;
+            if (__ballot(more) == 0ull) break;
+            float4 pq[kCoopStep];
+#pragma unroll
+            for (uint32_t u = 0; u < kCoopStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < kCoopStep; ++u)
+                if (i + u < i1 && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr)) mask |= 1u << u;
+            if (mask != 0u) {
+                my[cnt * kRB] = i | (mask << 24);  // spheres i + bit: resolve_pre's entry format
+                ++cnt;
+            }
+            i = more ? i + kCoopStep : i;
+            if (__ballot(cnt == (uint32_t)kCand) != 0ull) break;
+        }
+        ok = resolve_pre(S.cen, n, list, cnt, mk3(w[0], w[1], w[2]), mk3(w[3], w[4], w[5]), w[6], w[7], t_min,
+                         bc, bg) && ok;
+    } while (__ballot(i < i1) != 0ull);
     // c >= t_min > 0: its bits order like its value; ties -> larger index
     uint64_t key = bg >= 0 ? ((uint64_t)__float_as_uint(bc) << 32) | (uint64_t)(0xffffffffu - (uint32_t)bg)
                            : ~0ull;
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, s, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), s, 64);
+    for (uint32_t sh = g >> 1; sh != 0u; sh >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, (int)sh, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), (int)sh, 64);
         const uint64_t other = ((uint64_t)hi << 32) | lo;
         key = other < key ? other : key;
     }
-    if (key == ~0ull) return -1;
-    const float c = __uint_as_float((uint32_t)(key >> 32));
-    if (!(c <= best)) return -1;  // accepted iff c <= t_max (c < best, or c == best and index > -1)
+    const uint64_t badm = __ballot(!ok);
+    if (valid && k == 0u) {
+        const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
+        const uint64_t out = (badm & gm) != 0ull ? 0ull : key;  // 0: a non-finite root in the group
+        keys[2 * r] = (uint32_t)out;
+        keys[2 * r + 1] = (uint32_t)(out >> 32);
+    }
+    __builtin_amdgcn_wave_barrier();
+    seq = false;
+    if (!active) return -1;
+    const uint64_t kk = ((uint64_t)keys[2 * rank + 1] << 32) | keys[2 * rank];
+    if (kk == 0ull) {
+        seq = true;
+        return -1;
+    }
+    if (kk == ~0ull) return -1;
+    const float c = __uint_as_float((uint32_t)(kk >> 32));
+    if (!(c <= best)) return -1;  // accepted iff c <= t_max
     best = c;
-    return (int)(0xffffffffu - (uint32_t)key);
+    return (int)(0xffffffffu - (uint32_t)kk);
 }
 
 // Lane state: the pixel it is tracing and that pixel's current path.
@@ -538,6 +674,7 @@ struct Lane {
     float a, inv_a, seed;
     uint32_t sample, bounce, segs;
     uint32_t x, y, gid;  // pixel (global image coords) and its output slot
+    uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
     bool active;         // tracing a pixel
 };
 
@@ -716,9 +853,10 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
 }
 
 // Persistent-lane pixel queue: every idle lane of the wave takes the next
-// pixel index; ONE atomic per wave per refill (ballot + lane rank).
-// Returns true once the queue is exhausted (wave-uniform).
-__device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_t npix, Lane &L) {
+// slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
+// per refill (ballot + lane rank). Returns true once the queue is
+// exhausted (wave-uniform).
+__device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_t lo, uint32_t hi, Lane &L) {
     const uint64_t idle = __ballot(!L.active);
     if (idle == 0ull) return false;
     const uint32_t cnt = (uint32_t)__popcll(idle);
@@ -726,12 +864,61 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t base = 0;
     if ((int)lane == leader) base = atomicAdd(P.queue, cnt);
-    base = __shfl(base, leader, 64);
+    base = lo + __shfl(base, leader, 64);
     if (!L.active) {
         const uint32_t g = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-        if (g < npix) start_pixel(P, F, P.perm ? P.perm[g] : g, L);
+        if (g < hi) {
+            start_pixel(P, F, P.perm ? P.perm[g] : g, L);
+            L.slot = g;
+        }
     }
-    return base + cnt >= npix;
+    return base + cnt >= hi;
+}
+
+// Heavy pixels (the front of the cost-ordered queue, k_heavy_split) are
+// the frame's critical path: a pixel's samples are sequential (the
+// reference's RNG chain), so a pixel that costs more segments than a lane's
+// share of the frame cannot finish in lane mode however early it starts.
+// They are traced in group-coop mode (hit_world_groups), at a raised wave
+// priority, in two tiers: tier 1 = slots [0, k1), the very heaviest, up to
+// kHeavy1 per wave (64 / kHeavy1 lanes per ray: the shortest time per
+// segment); tier 2 = slots [k1, kh), up to kHeavy2 per wave. An idle wave
+// tries tier 1 first; a tier-2 wave tops itself up from tier 2. Returns the
+// wave's tier (0: not heavy any more).
+constexpr uint32_t kHeavy1 = RTX_HEAVY1_WAVE;
+constexpr uint32_t kHeavy2 = RTX_HEAVY_WAVE;
+struct HeavyState {
+    uint32_t k1, kh;     // tier ends
+    bool t1_done, t2_done;
+    uint32_t tier;       // 1, 2, or 0 (normal wave)
+};
+__device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint32_t *ctr, uint32_t lo, uint32_t hi,
+                                          uint32_t room, uint64_t act, Lane &L, bool &done) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t h = 0;
+    if (lane == 0u) h = atomicAdd(ctr, room);
+    h = lo + __shfl(h, 0, 64);
+    if (h >= hi) {
+        done = true;
+        return false;
+    }
+    const uint32_t take = min(room, hi - h);
+    const uint32_t rk = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
+    if (!L.active && rk < take) start_pixel(P, F, P.perm[h + rk], L);
+    if (h + room >= hi) done = true;
+    return true;
+}
+__device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, HeavyState &H, Lane &L) {
+    const uint64_t act = __ballot(L.active);
+    const uint32_t have = (uint32_t)__popcll(act);
+    if (have == 0u) H.tier = 0;
+    if (have == 0u && !H.t1_done && take_from(P, F, P.heavy, 0, H.k1, kHeavy1, act, L, H.t1_done)) {
+        H.tier = 1;
+        return;
+    }
+    if (H.tier == 1u) return;  // tier-1 waves keep to their few rays
+    if (!H.t2_done && have < kHeavy2 && take_from(P, F, P.heavy + 2, H.k1, H.kh, kHeavy2 - have, act, L, H.t2_done))
+        H.tier = 2;
 }
 
 // Render kernel, per-wave independent: RTX_SRC 0 keeps the sphere blocks
@@ -741,13 +928,24 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // otherwise an exact grid, one pixel per lane.
 template <bool kPersist>
 __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
-    // dynamic LDS: [candidate list, kListBytes][sphere blocks (RTX_SRC 0)]
+    // dynamic LDS: [candidate list, kListBytes][coop rays, kCoopBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
+    float *coop_ws = reinterpret_cast<float *>(s_mem + kListBytes) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
+    (void)coop_ws;
+#if RTX_SRC == 1
+    // the coop's sphere data: a block-wide LDS copy of pre4 for small scenes
+    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kListBytes + kCoopBytes);
+    const bool coop_lds = P.scene.n <= kCoopLds;
+    if (coop_lds) {
+        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) s_pre4[i] = P.scene.pre4[i];
+        __syncthreads();
+    }
+#endif
     const int last = (int)P.scene.n - 1;
 #if RTX_SRC == 0
     const uint32_t nblk = P.scene.n_pad / 8;
-    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
+    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes + kCoopBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kRB) s_blk4[i] = g4[i];
@@ -759,11 +957,20 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     Lane L;
     L.active = false;
     L.segs = 0;
+    L.slot = ~0u;
     bool exhausted = !kPersist;
     if (!kPersist) {
         const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
         if (gid < npix) start_pixel(P, F, gid, L);
     }
+    // heavy slots [0, kh) of the queue (k_heavy_split; tier 1 = [0, k1)), normal slots [kh, npix)
+    HeavyState H;
+    H.kh = (kPersist && P.heavy) ? min(P.heavy[1], npix) : 0u;
+    H.k1 = (kPersist && P.heavy) ? min(P.heavy[3], H.kh) : 0u;
+    H.t1_done = H.k1 == 0u;
+    H.t2_done = H.k1 == H.kh;
+    H.tier = 0;
+    const uint32_t kh = H.kh;
 #if RTX_DIAG_PROF
     // [0] refill clocks [1] hit_world [2] shade [3] tail mode [4] iterations [5] tail iterations
     // [6] active lanes summed over iterations
@@ -781,39 +988,37 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #define RTX_PROF(k)
 #endif
     for (;;) {
-        if (!exhausted) exhausted = refill(P, F, npix, L);
+        if (!(H.t1_done && H.t2_done) && (H.tier != 0u || __ballot(L.active) == 0ull)) take_heavy(P, F, H, L);
+        if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
+        const bool heavy = H.tier != 0u;
+        if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
         const uint64_t act = __ballot(L.active);
         RTX_PROF(0)
-        if (act == 0ull) break;  // spp, depth > 0: idle after refill => drained
+        if (act == 0ull) break;  // spp, depth > 0: idle after both queues => drained
 #if RTX_DIAG_PROF
         pr[4]++;
         pr[6] += __popcll(act);
 #endif
 #if RTX_SRC == 1
-        if (RTX_COOP_MAX && exhausted && __popcll(act) <= RTX_COOP_MAX) {
+        if (heavy || (RTX_COOP_MAX && exhausted && __popcll(act) <= RTX_COOP_MAX)) {
 #if RTX_DIAG_PROF
             pr[5]++;
 #endif
             // Frame tail: the few pixels left in this wave are its critical
-            // path; trace their rays one after another, each across all 64
-            // lanes, instead of all of them on one lane each.
+            // path; trace their rays together, several lanes per ray.
             float my_best = __uint_as_float(0x7f800000u);
-            int my_hit = -1;
             bool my_seq = false;
-            for (uint64_t m = act; m != 0ull; m &= m - 1ull) {
-                const int src = __ffsll((long long)m) - 1;
-                const f3 ro = mk3(read_lane(L.o.x, src), read_lane(L.o.y, src), read_lane(L.o.z, src));
-                const f3 rd = mk3(read_lane(L.d.x, src), read_lane(L.d.y, src), read_lane(L.d.z, src));
-                float b = __uint_as_float(0x7f800000u);
-                bool seq = false;
-                const int h = hit_world_coop(P.scene.soa, P.scene.n, ro, rd, read_lane(L.a, src),
-                                             read_lane(L.inv_a, src), kTMin, b, seq);
-                if ((int)(threadIdx.x & 63u) == src) {
-                    my_best = b;
-                    my_hit = h;
-                    my_seq = seq;
-                }
-            }
+            // this wave carries the frame's critical path: tier 1 > tier 2 > tail
+            if (H.tier == 1u)
+                __builtin_amdgcn_s_setprio(3);
+            else if (H.tier == 2u)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(RTX_TAIL_PRIO);
+            int my_hit = coop_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, act, L.active, L.o, L.d, L.a,
+                                                     L.inv_a, kTMin, coop_ws, list, my_best, my_seq)
+                                  : hit_world_groups(P.scene, P.scene.pre4, act, L.active, L.o, L.d, L.a, L.inv_a,
+                                                     kTMin, coop_ws, list, my_best, my_seq);
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
@@ -821,9 +1026,19 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 }
                 shade(P, F, L, min(my_hit, last), my_best);
             }
+            __builtin_amdgcn_s_setprio(0);
             RTX_PROF(3)
             continue;
         }
+#endif
+#if RTX_PRIO_FRAC_X100
+        // lane mode: a wave that holds one of the heaviest pixels of the
+        // normal queue (its first prio_slots slots) runs at the top priority,
+        // so its time per segment is not stretched by the SIMD's other waves
+        if (__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull)
+            __builtin_amdgcn_s_setprio(3);
+        else
+            __builtin_amdgcn_s_setprio(0);
 #endif
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
@@ -870,7 +1085,7 @@ __global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
     bool exhausted = false;
     constexpr uint32_t kChunkBlk = kChunk / 8;
     for (;;) {
-        if (!exhausted) exhausted = refill(P, F, npix, L);
+        if (!exhausted) exhausted = refill(P, F, 0, npix, L);
         if (!__syncthreads_or(L.active ? 1 : 0)) break;
         float best = __uint_as_float(0x7f800000u);
         int hit = -1;
@@ -960,6 +1175,34 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
         const uint32_t i = base + k * kBlock + threadIdx.x;
         if (i < n) perm[start[key[k]] + rank[k]] = i;
     }
+}
+
+// Heavy-pixel split: with key k ~ a pixel's cost, a lane's share of the
+// frame is W / lanes (W = sum of keys). Pixels whose key exceeds
+// RTX_HEAVY1_ALPHA times it form tier 1 (slots [0, k1): one pixel per wave,
+// 64 lanes per ray). When there are fewer pixels than RTX_HEAVY_RHO per
+// resident lane (a small share of a frame, e.g. one GPU's rows of an 8-GPU
+// split), the tier-1 bar rises to RTX_HEAVY1_ALPHA_SMALL times the share
+// and the pixels above RTX_HEAVY_ALPHA times it (up to that bar) form tier
+// 2 (slots [k1, kh), kHeavy2 per wave). Tiers and alphas were chosen with
+// tools/part_scaling.py on C2 split 1/2/4/8 ways. Writes kh to heavy[1] and
+// k1 to heavy[3]. One thread: 256 buckets.
+__global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t *heavy) {
+    if (threadIdx.x != 0u) return;
+    double w = 0.0;
+    for (uint32_t b = 0; b < kCostBuckets; ++b) w += (double)counts[b] * (double)(kCostBuckets - 1u - b);
+    const double share = w / (double)(lanes ? lanes : 1u);
+    const bool small = (double)npix < RTX_HEAVY_RHO * (double)lanes;
+    const double a1 = small ? RTX_HEAVY1_ALPHA_SMALL : RTX_HEAVY1_ALPHA;
+    const double a2 = small ? RTX_HEAVY_ALPHA : a1;
+    uint32_t kh = 0, k1 = 0;
+    for (uint32_t b = 0; b < kCostBuckets; ++b) {
+        const double key = (double)(kCostBuckets - 1u - b);
+        if (key > a2 * share) kh += counts[b];
+        if (key > a1 * share) k1 += counts[b];
+    }
+    heavy[1] = kh;
+    heavy[3] = k1;
 }
 
 // spp == 0 or depth == 0: no segment is traced; the pixel is
@@ -1072,7 +1315,7 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
     if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
-    const size_t lds = kListBytes + (RTX_SRC == 1 ? 0 : (size_t)p.scene.n_pad * sizeof(float4));
+    const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * sizeof(float4) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
     hipError_t e = allow_lds((const void *)k_render<false>, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render<false>, dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
@@ -1089,7 +1332,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     }
     hipError_t e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
-        const size_t lds = kListBytes + (RTX_SRC == 1 ? 0 : (size_t)p.scene.n_pad * sizeof(float4));
+        const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * sizeof(float4) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
         e = allow_lds((const void *)k_render<true>, lds);
         if (e == hipSuccess) e = allow_lds((const void *)k_render<false>, lds);
         if (e != hipSuccess) return e;
@@ -1106,7 +1349,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         c.counters = p.counters + 3;  // scratch: not part of the frame's segment count
         c.wave_times = nullptr;
         c.perm = nullptr;
-        e = hipMemsetAsync(sched.buckets, 0, 2 * kCostBuckets * sizeof(uint32_t), stream);
+        e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, c);
         // 2. counting sort by cost, descending
@@ -1115,12 +1358,16 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
                            p.rows_local, sched.buckets);
         hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                            p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
-        // 3. persistent render over the ordered queue
+        // 3. heavy-pixel split, then the persistent render over the ordered queue
+        const uint32_t blocks = min(need, resident_blocks((const void *)k_render<true>, lds));
+        uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
+        hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
         KParams q = p;
         q.perm = sched.perm;
+        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u);
+        q.heavy = RTX_HEAVY_WAVE ? heavy : nullptr;
         e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        const uint32_t blocks = min(need, resident_blocks((const void *)k_render<true>, lds));
         hipLaunchKernelGGL(k_render<true>, dim3(blocks), dim3(kRB), lds, stream, q);
     } else {
         const size_t lds = kListBytes + kChunk * sizeof(float4);
