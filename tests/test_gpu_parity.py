@@ -124,9 +124,10 @@ def test_hit_world_ties_and_padding(gpu_ctx, oracle, rtx):
 def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx):
     """Rays whose line passes within 1e-9..1e-2 (relative) of a sphere's
     silhouette, on either side, plus near-vertical rays (the prefilter's
-    degenerate basis), tiny and huge direction lengths and origins far down
-    the line: the kernel's prefiltered scan (rtx_prefilter.h) must return the
-    reference scan's records bit for bit."""
+    degenerate basis), tiny and huge direction lengths (some outside the
+    prefilter's safe range) and origins far down the line: the kernel's
+    prefiltered scan (rtx_prefilter.h) must return the reference scan's
+    records bit for bit."""
     rng = np.random.default_rng(11)
     world = rtx.random_world(11, depth=1, spp=1)
     sph = world.spheres.astype(np.float64)
@@ -143,7 +144,10 @@ def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx):
     delta = np.sign(rng.normal(size=n)) * 10.0 ** rng.uniform(-9, -2, n)
     p = c + (r * (1 + delta))[:, None] * e
     o = p - rng.uniform(-40, 40, n)[:, None] * dirs
-    d = dirs * (10.0 ** rng.uniform(-3, 3, n))[:, None]
+    scale = 10.0 ** rng.uniform(-3, 3, n)
+    ext = rng.random(n) < 0.05  # |d| outside the prefilter's safe range: lanes flag every sphere
+    scale[ext] = 10.0 ** rng.choice([-7.0, 7.0], ext.sum())
+    d = dirs * scale[:, None]
     rays = np.concatenate([o, d], 1).astype(np.float32)
     gpu_ctx.upload_world(world)
     got = gpu_ctx.debug_hit_world(rays)
@@ -300,6 +304,29 @@ def test_partitions_reassemble_bit_identical(gpu_ctx, rtx, nparts, tile_rows):
     assert_bits_equal(image.numpy(), full, f"{nparts} parts x {tile_rows}-row tiles")
     gathered.free()
     image.free()
+
+
+@pytest.mark.parametrize("nparts,part", [(8, 3), (4, 0), (2, 1)])
+def test_rank_share_of_c2_bit_exact(gpu_ctx, oracle, rtx, nparts, part):
+    """One rank's share of the C2 frame (rtx_render_rows with R parts): a
+    small share takes the heavy-pixel tiers (group-coop waves, k_heavy_split)
+    and the hot-wave priority; its rows must still equal the oracle's."""
+    W, H, T = 1920, 1080, 5
+    world = rtx.random_world(11, depth=50, spp=100)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(frame)
+    ids = rtx.part_row_ids(H, T, part, nparts)
+    buf = gpu_ctx.alloc((len(ids), W, 4))
+    gpu_ctx.stats_reset()
+    gpu_ctx.render_rows(T, part, nparts, buf.ptr)
+    st = gpu_ctx.stats()
+    got = buf.numpy()
+    buf.free()
+    pick = np.linspace(0, len(ids) - 1, 6).astype(int)
+    want, _ = oracle.render_rows(world, frame, ids[pick], nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(got[pick], want, f"part {part}/{nparts} rows")
+    assert st.samples == len(ids) * W * 100
 
 
 # ---------------------------------------------------------------------------
