@@ -45,13 +45,11 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof t1r10a3 t1r10a2 t1r10a3m2 r10
+VARIANTS := best prof ptime cprof
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
-VFLAGS_t1r10a3       := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=3.0 -DRTX_HEAVY1_ALPHA=3.0
-VFLAGS_t1r10a2       := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=2.0 -DRTX_HEAVY1_ALPHA=2.0
-VFLAGS_t1r10a3m2     := -DRTX_HEAVY_RHO=10.0 -DRTX_HEAVY_ALPHA=3.0 -DRTX_HEAVY1_ALPHA=3.0 -DRTX_HEAVY1_WAVE=2
-VFLAGS_r10           := -DRTX_HEAVY_RHO=10.0
+VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
+VFLAGS_cprof         := -DRTX_DIAG_COOP=1
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

@@ -59,6 +59,15 @@ enum { RTX_MAT_LAMBERT = 0, RTX_MAT_METAL = 1, RTX_MAT_DIELECTRIC = 2 };
  * behaviour. */
 enum { RTX_RNG_CHAIN = 0, RTX_RNG_PER_SAMPLE = 1 };
 
+/* rtx_frame.flags. RTX_FRAME_LAMBERT_GUARD (an extension):
+ * a diffuse scatter direction whose three components are all below 1e-9 in
+ * magnitude is replaced by the normal before it is normalised — the guard of
+ * the pixel-shader prototype's lambert (Shader_RT.fx:219-225) with the
+ * compute shader's own unused near_zero (ShaderCompute.hlsl:70-74). The
+ * compute shader has no guard (:209-217) and normalises a zero vector to
+ * NaN; 0 keeps that. */
+enum { RTX_FRAME_LAMBERT_GUARD = 1 };
+
 /* Scene (~ cbuffer b1 WorldDef, DxCSApp.cpp:64-71). Arrays are read during
  * rtx_upload_world and copied; the caller keeps ownership. Unlike the
  * reference's fixed 512-sphere cbuffer the count is unbounded. */
@@ -86,7 +95,8 @@ typedef struct rtx_frame {
     uint32_t height;          /* framebuffer height in pixels (texture Height, DxCSApp.cpp:330) */
     uint32_t rng_mode;        /* RTX_RNG_*; 0 = reference                     */
     uint32_t frame_index;     /* seed offset for progressive frames; 0 = reference (time unused, :296) */
-    uint32_t reserved[2];     /* must be 0 */
+    uint32_t flags;           /* RTX_FRAME_* bits; 0 = reference              */
+    uint32_t reserved;        /* must be 0 */
     /* Thin-lens defocus (an extension: the reference's compute
      * shader passes aperture but ignores it, DxCSApp.cpp:179 /
      * ShaderCompute.hlsl:118-127). lens_u/lens_v = camera u/v axes, lens_u[3]
@@ -201,6 +211,10 @@ RTX_API int rtx_scene_random_world(int32_t grid_half_extent, uint32_t capacity,
 /* WorldDef::test_world (DxCSApp.cpp:136-157): 4 spheres. */
 RTX_API int rtx_scene_test_world(float *spheres, float *mat_types,
                                  float *mat_values, uint32_t *count);
+/* The pixel-shader prototype's scene (Shader_RT.fx:300-335): 7 spheres
+ * (ground, 3 small Lambert, glass, Lambert, metal); arrays of capacity 7. */
+RTX_API int rtx_scene_ps_world(float *spheres, float *mat_types,
+                               float *mat_values, uint32_t *count);
 /* PerFrame::ComputeViewVals (DxCSApp.cpp:39-61) + the focus distance of
  * DxCSApp::Update (DxCSApp.cpp:488) with focus_dist <= 0 meaning
  * |from - at|. Fills the four view rows, img_w = width_px,
@@ -235,11 +249,15 @@ RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                 float t_min, float t_max, float *out);
 /* Evaluates device math function `fn` (RTX_FN_*) elementwise on host
  * arrays (in0, in1 may be unused); out receives n floats (hash functions
- * write 1, 2 or 3 floats per element: out must hold 3*n). Synchronous. */
+ * write 1, 2 or 3 floats per element: out must hold 3*n). The diffuse
+ * direction functions take n cases: in0 = p[3n], in1 = (normal, rius)[6n],
+ * out = normalize(((p + normal) + rius) - p)[3n] (ShaderCompute.hlsl:
+ * 211-212), unguarded or with RTX_FRAME_LAMBERT_GUARD. Synchronous. */
 enum {
     RTX_FN_SQRT = 0, RTX_FN_DIV = 1, RTX_FN_SIN = 2, RTX_FN_COS = 3,
     RTX_FN_LOG2 = 4, RTX_FN_EXP2 = 5, RTX_FN_POW = 6, RTX_FN_BASEHASH = 7,
-    RTX_FN_HASH1 = 8, RTX_FN_HASH2 = 9, RTX_FN_HASH3 = 10, RTX_FN_RIUS = 11
+    RTX_FN_HASH1 = 8, RTX_FN_HASH2 = 9, RTX_FN_HASH3 = 10, RTX_FN_RIUS = 11,
+    RTX_FN_LAMBERT_DIR = 12, RTX_FN_LAMBERT_DIR_GUARD = 13
 };
 RTX_API int rtx_debug_math(rtx_ctx *ctx, int fn, const float *in0,
                            const float *in1, uint32_t n, float *out);

@@ -45,7 +45,7 @@ protected:
     std::string m_error;
 };
 
-enum class SceneKind { RandomWorld, TestWorld };
+enum class SceneKind { RandomWorld, TestWorld, PsWorld };
 
 struct AppConfig {
     uint32_t width = 1024, height = 576;   // texture size, DxCSApp.cpp:330-331
@@ -62,6 +62,7 @@ struct AppConfig {
     bool simple_camera = false;            // Camera.h instead of ComputeViewVals
     float lens_aperture = 0.0f;            // > 0: thin lens (extension, §8f-3); 0 = reference pinhole
     uint32_t rng_mode = RTX_RNG_CHAIN;
+    bool lambert_guard = false;            // RTX_FRAME_LAMBERT_GUARD (extension, §8f-4); false = reference
 };
 
 class RtxCSApp : public RtxBase {

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liboracle.so")
 REF_GOLDEN = os.path.join(HERE, "_ref", "ref_golden")
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
-          hash1=8, hash2=9, hash3=10, rius=11)
+          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13)
 
 
 class or_world(C.Structure):
@@ -31,7 +31,8 @@ class or_frame(C.Structure):
                 ("vertical", C.c_float * 4), ("lower_left", C.c_float * 4),
                 ("img_w", C.c_float), ("img_h", C.c_float), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("rng_mode", C.c_uint32), ("frame_index", C.c_uint32),
-                ("reserved", C.c_uint32 * 2), ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
+                ("flags", C.c_uint32), ("reserved", C.c_uint32),
+                ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
 
 
 _lib = None
@@ -150,6 +151,18 @@ def math(fn: str, in0, in1=None):
     if lib().or_math(FN[fn], _f(a), _f(b) if b is not None else None, a.size, _f(out)) != 0:
         raise RuntimeError("or_math failed")
     return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
+
+
+def lambert_dir(p, nrm, rius, guard: bool):
+    """normalize(((p + normal) + rius) - p), optionally near-zero guarded
+    (RTX_FN_LAMBERT_DIR[_GUARD]); arrays of shape (n, 3)."""
+    a = np.ascontiguousarray(p, np.float32).reshape(-1, 3)
+    b = np.ascontiguousarray(np.concatenate([np.reshape(nrm, (-1, 3)), np.reshape(rius, (-1, 3))], 1), np.float32)
+    out = np.zeros_like(a)
+    fn = FN["lambert_dir_guard" if guard else "lambert_dir"]
+    if lib().or_math(fn, _f(a), _f(b), a.shape[0], _f(out)) != 0:
+        raise RuntimeError("or_math failed")
+    return out
 
 
 def base_hash(x: int, y: int) -> int:

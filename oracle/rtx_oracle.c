@@ -57,6 +57,13 @@ static inline v3f vnorm(v3f v) {
     const float inv = 1.0f / sqrtf(vdot(v, v));
     return vscale(inv, v);
 }
+/* RTX_FRAME_LAMBERT_GUARD: Shader_RT.fx:222-225 with near_zero of
+ * ShaderCompute.hlsl:70-74 (s = 1e-9). */
+static inline v3f lambert_guard32(v3f v, v3f nrm, uint32_t guard) {
+    const float s = 0.000000001f;
+    if (guard && fabsf(v.x) < s && fabsf(v.y) < s && fabsf(v.z) < s) return nrm;
+    return v;
+}
 
 /* ------------------------------------------------------------------------ */
 /* RNG, ShaderCompute.hlsl:23-48                                              */
@@ -204,6 +211,19 @@ static inline float to_gamma(float c) { return pow_rt(c, 0.454545454545f); }
 
 int or_math(int fn, const float *in0, const float *in1, uint32_t n, float *out) {
     if (!in0 || !out) return -1;
+    if (fn == 12 || fn == 13) { /* diffuse direction, ShaderCompute.hlsl:211-212 */
+        if (!in1) return -1;
+        for (uint32_t i = 0; i < n; ++i) {
+            const v3f p = v3(in0[3 * i], in0[3 * i + 1], in0[3 * i + 2]);
+            const v3f nrm = v3(in1[6 * i], in1[6 * i + 1], in1[6 * i + 2]);
+            const v3f r = v3(in1[6 * i + 3], in1[6 * i + 4], in1[6 * i + 5]);
+            const v3f d = vnorm(lambert_guard32(vsub(vadd(vadd(p, nrm), r), p), nrm, fn == 13));
+            out[3 * i] = d.x;
+            out[3 * i + 1] = d.y;
+            out[3 * i + 2] = d.z;
+        }
+        return 0;
+    }
     for (uint32_t i = 0; i < n; ++i) {
         const float a = in0[i];
         const float b = in1 ? in1[i] : 0.0f;
@@ -355,7 +375,7 @@ int or_hit_world_f32(const or_world *w, const float *rays, uint32_t nr, float t_
 typedef struct {
     v3f org, hor, ver, llc;
     float img_w, img_h;
-    uint32_t width, rng_mode, frame_index;
+    uint32_t width, rng_mode, frame_index, flags;
     v3f lu, lv;
     float lens_r;
     int linear; /* 1: write the linear sample sum instead of toGamma(sum/spp) */
@@ -408,7 +428,7 @@ static void pixel32(const scene32 *S, const frame32 *F, uint32_t x, uint32_t y, 
                 if (mt == 0) {
                     const v3f r = rius(&seed);
                     const v3f target = vadd(vadd(p, nrm), r);
-                    dir = vnorm(vsub(target, p));
+                    dir = vnorm(lambert_guard32(vsub(target, p), nrm, F->flags & 1u));
                     col = vmul(col, v3(mv[0], mv[1], mv[2]));
                 } else if (mt == 1) {
                     const v3f refl = reflect3(d, nrm);
@@ -612,7 +632,9 @@ static void pixel64(const scene64 *S, const frame32 *F, uint32_t x, uint32_t y, 
                     const double r = pow(hh.z, 1.0 / 3.0), sq = sqrt(1.0 - hx * hx);
                     const v3d rr = d3(r * sq * sin(phi), r * sq * cos(phi), r * hx);
                     if (mt == 0) {
-                        dir = dunit(dsub(dadd(dadd(p, nrm), rr), p));
+                        v3d v = dsub(dadd(dadd(p, nrm), rr), p);
+                        if ((F->flags & 1u) && fabs(v.x) < 1e-9 && fabs(v.y) < 1e-9 && fabs(v.z) < 1e-9) v = nrm;
+                        dir = dunit(v);
                     } else {
                         const v3d refl = dsub(d, dscale(2.0 * ddot(d, nrm), nrm));
                         dir = dunit(dadd(refl, dscale(mv[3], rr)));
@@ -715,6 +737,7 @@ static int render_rows_impl(const or_world *w, const or_frame *f, const uint32_t
     F.width = f->width;
     F.rng_mode = f->rng_mode;
     F.frame_index = f->frame_index;
+    F.flags = f->flags;
     F.lu = v3(f->lens_u[0], f->lens_u[1], f->lens_u[2]);
     F.lv = v3(f->lens_v[0], f->lens_v[1], f->lens_v[2]);
     F.lens_r = f->lens_u[3];

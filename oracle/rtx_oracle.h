@@ -36,7 +36,7 @@ typedef struct or_world {
 typedef struct or_frame {
     float origin[4], horizontal[4], vertical[4], lower_left[4];
     float img_w, img_h;
-    uint32_t width, height, rng_mode, frame_index, reserved[2];
+    uint32_t width, height, rng_mode, frame_index, flags, reserved; /* flags: RTX_FRAME_* */
     float lens_u[4], lens_v[4]; /* thin lens: axes, lens_u[3] = radius (0 = pinhole) */
 } or_frame;
 
@@ -63,7 +63,8 @@ int or_hit_world_f64(const double *spheres /* 4*count */, uint32_t count, const 
 int or_camera_simple_rays_f64(uint32_t width, uint32_t height, const double *uv, uint32_t n,
                               double *out);
 
-/* Elementwise math of the twin spec; fn codes = RTX_FN_* of include/rtx.h. */
+/* Elementwise math of the twin spec; fn codes = RTX_FN_* of include/rtx.h
+ * (12/13, the diffuse direction: in0 = p[3n], in1 = (normal, rius)[6n]). */
 int or_math(int fn, const float *in0, const float *in1, uint32_t n, float *out);
 uint32_t or_base_hash(uint32_t x, uint32_t y);
 

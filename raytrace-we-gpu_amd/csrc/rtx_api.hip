@@ -289,6 +289,8 @@ int rtx_set_frame(rtx_ctx *c, const rtx_frame *f) {
     if (f->width == 0 || f->height == 0)
         return fail(RTX_ERR_INVALID, "rtx_set_frame: zero width or height");
     if (f->rng_mode > 1) return fail(RTX_ERR_INVALID, "rtx_set_frame: unknown rng_mode");
+    if ((f->flags & ~(uint32_t)RTX_FRAME_LAMBERT_GUARD) != 0 || f->reserved != 0)
+        return fail(RTX_ERR_INVALID, "rtx_set_frame: unknown flags or nonzero reserved");
     if (!(f->lens_u[3] >= 0.0f)) return fail(RTX_ERR_INVALID, "rtx_set_frame: negative lens radius");
     if ((uint64_t)f->width * f->height > (1ull << 31))
         return fail(RTX_ERR_INVALID, "rtx_set_frame: more than 2^31 pixels");
@@ -357,6 +359,7 @@ static rtx::KParams make_params(const rtx_ctx *c, uint32_t rows, uint32_t tile_r
     p.nparts = nparts;
     p.rng_mode = f.rng_mode;
     p.frame_index = frame_index;
+    p.flags = f.flags;
     p.accum = accum;
     p.accum_frames = accum_frames;
     for (int k = 0; k < 3; ++k) {
@@ -365,6 +368,7 @@ static rtx::KParams make_params(const rtx_ctx *c, uint32_t rows, uint32_t tile_r
     }
     p.lens_r = f.lens_u[3];
     p.wave_times = c->d_wave_times;
+    p.wave_cap = (uint32_t)std::min<size_t>(c->wave_times_cap, 0xffffffffu);
     for (int k = 0; k < 3; ++k) {
         p.org[k] = f.origin[k];
         p.hor[k] = f.horizontal[k];
@@ -616,17 +620,21 @@ int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_m
 
 int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint32_t n, float *out) {
     if (!c || (n && (!in0 || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_math: null argument");
-    if (fn < RTX_FN_SQRT || fn > RTX_FN_RIUS) return fail(RTX_ERR_INVALID, "rtx_debug_math: unknown fn");
+    if (fn < RTX_FN_SQRT || fn > RTX_FN_LAMBERT_DIR_GUARD)
+        return fail(RTX_ERR_INVALID, "rtx_debug_math: unknown fn");
+    const bool vec = fn >= RTX_FN_LAMBERT_DIR;  // in0 = p[3n], in1 = (normal, rius)[6n]
+    if (vec && n && !in1) return fail(RTX_ERR_INVALID, "rtx_debug_math: lambert functions need in1");
     if (n == 0) return RTX_OK;
     int rc = set_device(c);
     if (rc) return rc;
     float *d0 = nullptr, *d1 = nullptr, *dout = nullptr;
     const size_t outn = (size_t)n * 3;
-    RTX_HIP(hipMalloc(&d0, (size_t)n * sizeof(float)));
+    const size_t n0 = vec ? (size_t)n * 3 : (size_t)n, n1 = vec ? (size_t)n * 6 : (size_t)n;
+    RTX_HIP(hipMalloc(&d0, n0 * sizeof(float)));
     hipError_t e = hipMalloc(&dout, outn * sizeof(float));
-    if (e == hipSuccess && in1) e = hipMalloc(&d1, (size_t)n * sizeof(float));
-    if (e == hipSuccess) e = hipMemcpyAsync(d0, in0, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess && in1) e = hipMemcpyAsync(d1, in1, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && in1) e = hipMalloc(&d1, n1 * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpyAsync(d0, in0, n0 * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && in1) e = hipMemcpyAsync(d1, in1, n1 * sizeof(float), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(dout, 0, outn * sizeof(float), c->stream);
     if (e == hipSuccess) e = rtx::launch_debug_math(fn, d0, d1, n, dout, c->stream);
     const size_t copy_n = (fn >= RTX_FN_HASH1) ? outn : (size_t)n;

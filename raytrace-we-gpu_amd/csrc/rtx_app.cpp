@@ -38,7 +38,7 @@ RtxCSApp::~RtxCSApp() { Terminate(); }
 
 bool RtxCSApp::LoadContent() {
     // WorldDef w; WorldDef::random_world(w);  (DxCSApp.cpp:401-402)
-    uint32_t cap = 4;
+    uint32_t cap = m_cfg.scene == SceneKind::PsWorld ? 7 : 4;
     if (m_cfg.scene == SceneKind::RandomWorld) {
         const uint64_t full = 4ull + 4ull * (uint64_t)m_cfg.grid_half_extent * m_cfg.grid_half_extent;
         cap = (uint32_t)std::min<uint64_t>(full, m_cfg.max_spheres ? m_cfg.max_spheres : full);
@@ -49,8 +49,10 @@ bool RtxCSApp::LoadContent() {
     int rc = (m_cfg.scene == SceneKind::RandomWorld)
                  ? rtx_scene_random_world(m_cfg.grid_half_extent, cap, m_spheres.data(),
                                           m_mat_types.data(), m_mat_values.data(), &m_count)
-                 : rtx_scene_test_world(m_spheres.data(), m_mat_types.data(), m_mat_values.data(),
-                                        &m_count);
+                 : (m_cfg.scene == SceneKind::PsWorld)
+                       ? rtx_scene_ps_world(m_spheres.data(), m_mat_types.data(), m_mat_values.data(), &m_count)
+                       : rtx_scene_test_world(m_spheres.data(), m_mat_types.data(), m_mat_values.data(),
+                                              &m_count);
     if (rc != RTX_OK) {
         m_error = "scene generation failed";
         return m_ok = false;
@@ -87,6 +89,7 @@ void RtxCSApp::Update() {
         rc = rtx_camera_look_at(m_cfg.cam_pos, m_cfg.cam_look_at, m_cfg.up, m_cfg.vfov, m_cfg.aspect,
                                 m_cfg.aperture, 0.0f, m_cfg.width, m_cfg.height, &m_frame);
     m_frame.rng_mode = m_cfg.rng_mode;
+    m_frame.flags = m_cfg.lambert_guard ? RTX_FRAME_LAMBERT_GUARD : 0u;
     if (rc == RTX_OK && m_cfg.lens_aperture > 0.0f) rc = rtx_camera_set_aperture(&m_frame, m_cfg.lens_aperture);
     ++m_frame_count;
     if (rc != RTX_OK || rtx_set_frame(m_ctx, &m_frame) != RTX_OK) {

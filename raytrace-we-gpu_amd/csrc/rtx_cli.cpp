@@ -4,12 +4,13 @@
 // writes the last frame as PFM / PPM.
 //
 //   rtx_cli [--width W] [--height H] [--spp S] [--depth D]
-//           [--scene rtiow9|rtiow11|test|random:EXT[:MAX]] [--simple-camera]
+//           [--scene rtiow9|rtiow11|test|ps|random:EXT[:MAX]] [--simple-camera]
 //           [--rng chain|per-sample] [--frames K] [--device N]
-//           [--aperture A] [--accumulate]
+//           [--aperture A] [--accumulate] [--lambert-guard]
 //           [--pfm out.pfm] [--ppm out.ppm]
 // --accumulate renders the K frames progressively (rtx_accumulate) instead
-// of K independent frames; --aperture enables the thin lens.
+// of K independent frames; --aperture enables the thin lens;
+// --lambert-guard the near-zero diffuse guard (RTX_FRAME_LAMBERT_GUARD).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -22,9 +23,9 @@
 static void usage() {
     std::fprintf(stderr,
                  "usage: rtx_cli [--width W] [--height H] [--spp S] [--depth D]\n"
-                 "               [--scene rtiow9|rtiow11|test|random:EXT[:MAX]] [--simple-camera]\n"
+                 "               [--scene rtiow9|rtiow11|test|ps|random:EXT[:MAX]] [--simple-camera]\n"
                  "               [--rng chain|per-sample] [--frames K] [--device N]\n"
-                 "               [--aperture A] [--accumulate] [--pfm FILE] [--ppm FILE]\n");
+                 "               [--aperture A] [--accumulate] [--lambert-guard] [--pfm FILE] [--ppm FILE]\n");
 }
 
 int main(int argc, char **argv) {
@@ -57,6 +58,7 @@ int main(int argc, char **argv) {
         else if (a == "--simple-camera") cfg.simple_camera = true;
         else if (a == "--aperture") cfg.lens_aperture = (float)std::atof(next());
         else if (a == "--accumulate") accumulate = true;
+        else if (a == "--lambert-guard") cfg.lambert_guard = true;
         else if (a == "--rng") {
             const std::string m = next();
             cfg.rng_mode = (m == "per-sample") ? RTX_RNG_PER_SAMPLE : RTX_RNG_CHAIN;
@@ -65,6 +67,7 @@ int main(int argc, char **argv) {
             if (s == "rtiow9") cfg.grid_half_extent = 9;
             else if (s == "rtiow11") cfg.grid_half_extent = 11;
             else if (s == "test") cfg.scene = rtx::SceneKind::TestWorld;
+            else if (s == "ps") cfg.scene = rtx::SceneKind::PsWorld;
             else if (s.rfind("random:", 0) == 0) {
                 unsigned ext = 0, mx = 0;
                 if (std::sscanf(s.c_str() + 7, "%u:%u", &ext, &mx) < 1) {

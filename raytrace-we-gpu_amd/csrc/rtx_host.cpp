@@ -123,6 +123,27 @@ int rtx_scene_test_world(float *spheres, float *mat_types, float *mat_values, ui
     return RTX_OK;
 }
 
+// The pixel-shader prototype's scene (Shader_RT.fx:300-335, its
+// random_world, whose loop was never finished: ":310 TODO: debug why loops +
+// randoms don't work"): the ground, three small Lambert spheres and the
+// three big ones. Materials in this library's encoding (mat_values .w =
+// fuzz or ir; the prototype's -1 placeholders kept where unused). Rendered
+// with the compute shader's material semantics (the prototype's own
+// hemisphere sampling and by-value RNG are out of scope).
+int rtx_scene_ps_world(float *spheres, float *mat_types, float *mat_values, uint32_t *count) {
+    if (!spheres || !mat_types || !mat_values || !count) return RTX_ERR_INVALID;
+    Writer w{spheres, mat_types, mat_values, 7};
+    w.put(0.0f, -1000.0f, 0.0f, 1000.0f, 0.0f, 0.5f, 0.5f, 0.5f, -1.0f);  // :306 AddLambert
+    w.put(3.0f, 0.2f, 1.5f, 0.2f, 0.0f, 0.2f, 0.2f, 0.8f, -1.0f);         // :311
+    w.put(4.5f, 0.2f, 1.0f, 0.2f, 0.0f, 0.2f, 0.8f, 0.2f, -1.0f);         // :315
+    w.put(4.5f, 0.2f, 2.0f, 0.2f, 0.0f, 0.8f, 0.3f, 0.2f, -1.0f);         // :319
+    w.put(0.0f, 1.0f, 0.0f, 1.0f, 2.0f, 1.0f, 1.0f, 1.0f, 1.5f);          // :323 AddDielectric
+    w.put(-4.0f, 1.0f, 0.0f, 1.0f, 0.0f, 0.4f, 0.2f, 0.1f, -1.0f);        // :326
+    w.put(4.0f, 1.0f, 0.0f, 1.0f, 1.0f, 0.7f, 0.6f, 0.5f, 0.0f);          // :329 AddMetal, fuzz 0
+    *count = w.count;
+    return RTX_OK;
+}
+
 // PerFrame::ComputeViewVals (DxCSApp.cpp:39-61) with the focus distance of
 // DxCSApp::Update (:488). The aperture is passed but unused, as in the
 // reference (:179; get_ray ignores it, ShaderCompute.hlsl:118-127).

@@ -35,6 +35,8 @@ struct KScene {
 
 constexpr uint32_t kPad = 8;  // spheres per AoSoA block
 
+constexpr uint32_t kFrameLambertGuard = 1u;  // = RTX_FRAME_LAMBERT_GUARD
+
 // Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
 struct KParams {
     KScene scene;
@@ -45,12 +47,14 @@ struct KParams {
     uint32_t width, rows_local;    // launch covers rows_local * width lanes
     uint32_t tile_rows, part, nparts;
     uint32_t rng_mode, frame_index;
+    uint32_t flags;                // kFrame* bits (rtx_frame.flags)
     float org[3], hor[3], ver[3], llc[3];
     float img_w, img_h;
     float lens_u[3], lens_v[3], lens_r;  // thin lens (lens_r 0 = pinhole)
     float4 *accum;                 // progressive accumulation (NULL = plain frame)
     uint32_t accum_frames;         // frames in accum after this launch
     unsigned long long *wave_times;  // diagnostic: per-wave (start, end) s_memrealtime, or NULL
+    uint32_t wave_cap;             // pairs in wave_times
     const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority

@@ -83,6 +83,12 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
 #define RTX_DIAG_PROF 0
 #endif
+#ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
+#define RTX_DIAG_PIXEL 0
+#endif
+#ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-1 coop segments into wave_times[0..7]
+#define RTX_DIAG_COOP 0
+#endif
 #ifndef RTX_SHADE_MERGE  // 1: Lambert and metal lanes share one scatter path
 #define RTX_SHADE_MERGE 1
 #endif
@@ -580,7 +586,14 @@ static_assert(RTX_COOP_MAX <= (int)kCoopSlots, "RTX_COOP_MAX must be <= 32");
 template <typename Q4>
 __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64_t act, bool active, f3 o,
                                                 f3 d, float a, float inv_a, float t_min, float *ws,
-                                                uint32_t *list, float &best, bool &seq) {
+                                                uint32_t *list, float &best, bool &seq,
+                                                unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
+#define RTX_CP(k)                                                   \
+    if (RTX_DIAG_COOP && cp) {                                      \
+        const unsigned long long tn = __builtin_readcyclecounter(); \
+        cp[k] += tn - *tq;                                          \
+        *tq = tn;                                                   \
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m = (uint32_t)__popcll(act);
     const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
@@ -604,6 +617,7 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
     const bool valid = r < m;
     const float *w = ws + 8 * (valid ? r : 0u);  // the group's ray (re-read where needed: fewer live VGPRs)
     const LineTest T = line_test_setup(w[0], w[1], w[2], w[3], w[4], w[5], w[6], S.smag);
+    RTX_CP(0)
     const uint32_t n = S.n;
     // lane k of a group scans the contiguous chunk [k*ch, k*ch + ch) of the
     // spheres (ch odd, so the group's LDS reads fall in different banks),
@@ -637,6 +651,7 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
         ok = resolve_pre(S.cen, n, list, cnt, mk3(w[0], w[1], w[2]), mk3(w[3], w[4], w[5]), w[6], w[7], t_min,
                          bc, bg) && ok;
     } while (__ballot(i < i1) != 0ull);
+    RTX_CP(1)
     // c >= t_min > 0: its bits order like its value; ties -> larger index
     uint64_t key = bg >= 0 ? ((uint64_t)__float_as_uint(bc) << 32) | (uint64_t)(0xffffffffu - (uint32_t)bg)
                            : ~0ull;
@@ -654,6 +669,7 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
         keys[2 * r + 1] = (uint32_t)(out >> 32);
     }
     __builtin_amdgcn_wave_barrier();
+    RTX_CP(2)
     seq = false;
     if (!active) return -1;
     const uint64_t kk = ((uint64_t)keys[2 * rank + 1] << 32) | keys[2 * rank];
@@ -733,6 +749,16 @@ __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
     P.out[L.gid] = o;
 }
 
+// Diffuse direction before normalisation, target - p (ShaderCompute.hlsl:
+// 211-212), with the optional near-zero guard (RTX_FRAME_LAMBERT_GUARD,
+// §8f-4): the prototype's lambert (Shader_RT.fx:222-225) with the compute
+// shader's unused near_zero (ShaderCompute.hlsl:70-74, s = 1e-9).
+__device__ __forceinline__ f3 lambert_guard(f3 v, f3 nrm, bool guard) {
+    const float s = 0.000000001f;
+    const bool nz = fabsf(v.x) < s && fabsf(v.y) < s && fabsf(v.z) < s;
+    return guard && nz ? nrm : v;
+}
+
 __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
     L.segs++;
     bool ended = false;
@@ -755,14 +781,14 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
             const f3 rius = random_in_unit_sphere(L.seed);
             const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
                                  : reflect3(L.d, nrm) + mv.w * rius;     // METAL (:219-227)
-            dir = normalize3(v);
+            dir = normalize3(lambert_guard(v, nrm, mt == 0 && (P.flags & kFrameLambertGuard) != 0u));
             L.col = L.col * mk3(mv.x, mv.y, mv.z);
         } else if (mt == 2) {
 #else
         if (mt == 0) {  // DIFFUSE (:209-217)
             const f3 rius = random_in_unit_sphere(L.seed);
             const f3 target = (p + nrm) + rius;
-            dir = normalize3(target - p);
+            dir = normalize3(lambert_guard(target - p, nrm, (P.flags & kFrameLambertGuard) != 0u));
             L.col = L.col * mk3(mv.x, mv.y, mv.z);
         } else if (mt == 1) {  // METAL (:219-227), always scatters
             const f3 refl = reflect3(L.d, nrm);
@@ -805,6 +831,9 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
         if (L.sample >= P.spp) {
             write_pixel(P, L);
             L.active = false;
+#if RTX_DIAG_PIXEL
+            if (P.wave_times && L.gid < P.wave_cap) P.wave_times[2 * L.gid + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
         } else {
             begin_sample(P, F, L.x, L.y, L);
         }
@@ -870,6 +899,9 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
         if (g < hi) {
             start_pixel(P, F, P.perm ? P.perm[g] : g, L);
             L.slot = g;
+#if RTX_DIAG_PIXEL
+            if (P.wave_times && L.gid < P.wave_cap) P.wave_times[2 * L.gid] = __builtin_amdgcn_s_memrealtime() << 2;
+#endif
         }
     }
     return base + cnt >= hi;
@@ -904,7 +936,13 @@ __device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint
     }
     const uint32_t take = min(room, hi - h);
     const uint32_t rk = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
-    if (!L.active && rk < take) start_pixel(P, F, P.perm[h + rk], L);
+    if (!L.active && rk < take) {
+        start_pixel(P, F, P.perm[h + rk], L);
+#if RTX_DIAG_PIXEL
+        if (P.wave_times && L.gid < P.wave_cap)
+            P.wave_times[2 * L.gid] = (__builtin_amdgcn_s_memrealtime() << 2) | (ctr == P.heavy ? 1ull : 2ull);
+#endif
+    }
     if (h + room >= hi) done = true;
     return true;
 }
@@ -987,6 +1025,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #else
 #define RTX_PROF(k)
 #endif
+#if RTX_DIAG_COOP
+    // tier-1 coop segments: [0] ray exchange + line setup [1] scan + resolve
+    // [2] reduction [3] shade [4] loop overhead [5] segments
+    unsigned long long cpa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ctq = __builtin_readcyclecounter();
+    bool was_t1 = false;
+#endif
     for (;;) {
         if (!(H.t1_done && H.t2_done) && (H.tier != 0u || __ballot(L.active) == 0ull)) take_heavy(P, F, H, L);
         if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
@@ -1015,10 +1060,22 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(RTX_TAIL_PRIO);
+#if RTX_DIAG_COOP
+            unsigned long long *cp = H.tier == 1u ? cpa : nullptr;
+            unsigned long long *ctqp = &ctq;
+            if (H.tier == 1u) {
+                const unsigned long long tn = __builtin_readcyclecounter();
+                if (was_t1) cpa[4] += tn - ctq;
+                ctq = tn;
+                cpa[5]++;
+            }
+#else
+            unsigned long long *cp = nullptr, *ctqp = nullptr;
+#endif
             int my_hit = coop_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, act, L.active, L.o, L.d, L.a,
-                                                     L.inv_a, kTMin, coop_ws, list, my_best, my_seq)
+                                                     L.inv_a, kTMin, coop_ws, list, my_best, my_seq, cp, ctqp)
                                   : hit_world_groups(P.scene, P.scene.pre4, act, L.active, L.o, L.d, L.a, L.inv_a,
-                                                     kTMin, coop_ws, list, my_best, my_seq);
+                                                     kTMin, coop_ws, list, my_best, my_seq, cp, ctqp);
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
@@ -1026,6 +1083,14 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 }
                 shade(P, F, L, min(my_hit, last), my_best);
             }
+#if RTX_DIAG_COOP
+            if (cp) {
+                const unsigned long long tn = __builtin_readcyclecounter();
+                cpa[3] += tn - ctq;
+                ctq = tn;
+            }
+            was_t1 = H.tier == 1u;
+#endif
             __builtin_amdgcn_s_setprio(0);
             RTX_PROF(3)
             continue;
@@ -1058,8 +1123,12 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     if (P.wave_times && (threadIdx.x & 63u) == 0u)
         for (int k = 0; k < 5; ++k) atomicAdd(&P.wave_times[8 + k], (unsigned long long)diag_slots()[k]);
 #endif
+#if RTX_DIAG_COOP
+    if (P.wave_times && (threadIdx.x & 63u) == 0u)
+        for (int k = 0; k < 6; ++k) atomicAdd(&P.wave_times[k], cpa[k]);
+#endif
     count_segments(P, L.segs);
-    if (!RTX_DIAG_PROF && P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
+    if (!RTX_DIAG_PROF && !RTX_DIAG_PIXEL && !RTX_DIAG_COOP && P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
         const uint32_t w = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
         P.wave_times[2 * w] = t_start;
         P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1267,6 +1336,16 @@ __global__ void __launch_bounds__(kBlock) k_debug_math(int fn, const float *in0,
                                                        uint32_t n, float *out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
+    if (fn == 12 || fn == 13) {  // diffuse direction: in0 = p[3n], in1 = (normal, rius)[6n]
+        const f3 p = mk3(in0[3 * i], in0[3 * i + 1], in0[3 * i + 2]);
+        const f3 nrm = mk3(in1[6 * i], in1[6 * i + 1], in1[6 * i + 2]);
+        const f3 rius = mk3(in1[6 * i + 3], in1[6 * i + 4], in1[6 * i + 5]);
+        const f3 dir = normalize3(lambert_guard(((p + nrm) + rius) - p, nrm, fn == 13));
+        out[3 * i] = dir.x;
+        out[3 * i + 1] = dir.y;
+        out[3 * i + 2] = dir.z;
+        return;
+    }
     const float a = in0[i];
     const float b = in1 ? in1[i] : 0.0f;
     float seed = a;

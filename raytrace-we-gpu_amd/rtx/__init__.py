@@ -29,7 +29,8 @@ RTX_OK = 0
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
-          hash1=8, hash2=9, hash3=10, rius=11)
+          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13)
+FRAME_LAMBERT_GUARD = 1  # rtx_frame.flags bit (RTX_FRAME_LAMBERT_GUARD)
 
 
 class RtxError(RuntimeError):
@@ -47,7 +48,8 @@ class rtx_frame(C.Structure):
                 ("vertical", C.c_float * 4), ("lower_left", C.c_float * 4),
                 ("img_w", C.c_float), ("img_h", C.c_float), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("rng_mode", C.c_uint32), ("frame_index", C.c_uint32),
-                ("reserved", C.c_uint32 * 2), ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
+                ("flags", C.c_uint32), ("reserved", C.c_uint32),
+                ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
 
 
 class rtx_stats(C.Structure):
@@ -97,6 +99,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_get_stats": (C.c_int, [ctx, C.POINTER(rtx_stats)]),
         "rtx_scene_random_world": (C.c_int, [i32, u32, f, f, f, C.POINTER(u32)]),
         "rtx_scene_test_world": (C.c_int, [f, f, f, C.POINTER(u32)]),
+        "rtx_scene_ps_world": (C.c_int, [f, f, f, C.POINTER(u32)]),
         "rtx_camera_look_at": (C.c_int, [f, f, f, C.c_float, C.c_float, C.c_float, C.c_float,
                                          u32, u32, C.POINTER(rtx_frame)]),
         "rtx_camera_simple": (C.c_int, [u32, u32, C.POINTER(rtx_frame)]),
@@ -177,6 +180,18 @@ def test_world(depth: int = 50, spp: int = 50) -> World:
     n = C.c_uint32()
     _check(load_library().rtx_scene_test_world(_fptr(sph), _fptr(mt), _fptr(mv), C.byref(n)),
            "rtx_scene_test_world")
+    return World(sph, mt, mv, depth, spp)
+
+
+def ps_world(depth: int = 25, spp: int = 1) -> World:
+    """The pixel-shader prototype's 7-sphere scene (Shader_RT.fx:300-335);
+    its defaults depth 25, 1 sample (Shader_RT.fx:392, 430)."""
+    sph = np.zeros((7, 4), np.float32)
+    mt = np.zeros(7, np.float32)
+    mv = np.zeros((7, 4), np.float32)
+    n = C.c_uint32()
+    _check(load_library().rtx_scene_ps_world(_fptr(sph), _fptr(mt), _fptr(mv), C.byref(n)),
+           "rtx_scene_ps_world")
     return World(sph, mt, mv, depth, spp)
 
 
@@ -346,6 +361,18 @@ class Context:
                                         _fptr(b) if b is not None else None, a.size, _fptr(out)),
                "rtx_debug_math")
         return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
+
+    def debug_lambert_dir(self, p: np.ndarray, nrm: np.ndarray, rius: np.ndarray, guard: bool) -> np.ndarray:
+        """The kernel's diffuse direction, normalize(((p + normal) + rius) - p),
+        optionally near-zero guarded (RTX_FN_LAMBERT_DIR[_GUARD]); (n, 3) arrays."""
+        a = np.ascontiguousarray(p, np.float32).reshape(-1, 3)
+        b = np.ascontiguousarray(np.concatenate([np.reshape(nrm, (-1, 3)), np.reshape(rius, (-1, 3))], 1),
+                                 np.float32)
+        out = np.zeros_like(a)
+        fn = FN["lambert_dir_guard" if guard else "lambert_dir"]
+        _check(self._lib.rtx_debug_math(self._h, fn, _fptr(a), _fptr(b), a.shape[0], _fptr(out)),
+               "rtx_debug_math")
+        return out
 
 
 class DeviceArray:

@@ -197,6 +197,46 @@ def test_random_world_frames_bit_exact(gpu_ctx, oracle, rtx, ext, w, h, spp, dep
     assert st.sphere_tests == segs * world.count
 
 
+def test_lambert_guard_device(gpu_ctx, oracle):
+    """RTX_FN_LAMBERT_DIR[_GUARD]: the kernel's diffuse direction equals the
+    oracle's bit for bit; zero directions give NaN unguarded, the normal guarded."""
+    from test_oracle_golden import lambert_cases
+    p, nrm, rius, nz = lambert_cases()
+    for guard in (False, True):
+        got = gpu_ctx.debug_lambert_dir(p, nrm, rius, guard)
+        want = oracle.lambert_dir(p, nrm, rius, guard)
+        assert_bits_equal(got[:-nz], want[:-nz], f"lambert guard={guard}")
+        if guard:
+            assert_bits_equal(got[-nz:], nrm[-nz:], "guarded zero directions")
+        else:
+            assert np.isnan(got[-nz:]).all()
+
+
+def test_lambert_guard_frame_bit_exact(gpu_ctx, oracle, rtx):
+    world = rtx.random_world(9, depth=20, spp=3)
+    frame = rtx.camera_look_at(96, 54, aspect=96 / 54)
+    frame.flags = rtx.FRAME_LAMBERT_GUARD
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(54), nthreads=8)
+    assert_bits_equal(img, want, "lambert-guard frame")
+    assert st.segments == segs
+    bad = rtx.camera_look_at(96, 54, aspect=96 / 54)
+    bad.flags = 2
+    with pytest.raises(rtx.RtxError):
+        gpu_ctx.set_frame(bad)
+
+
+@pytest.mark.parametrize("spp,depth", [(1, 25), (8, 25)])
+def test_ps_world_bit_exact(gpu_ctx, oracle, rtx, spp, depth):
+    """f-4: the pixel-shader prototype's 7-sphere scene (Shader_RT.fx:300-335)
+    at its own depth 25, through the compute path, every pixel bit-exact."""
+    world = rtx.ps_world(depth=depth, spp=spp)
+    frame = rtx.camera_look_at(320, 180)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(180), nthreads=8)
+    assert_bits_equal(img, want, f"ps_world spp {spp}")
+    assert st.segments == segs
+
 def test_c2_full_size_row_subset(gpu_ctx, oracle, rtx):
     """C2 at full size: 1920x1080, RTIOW final scene (486 spheres), spp 100,
     depth 50. The oracle renders every 24th row (45 rows, 8.6 M samples);

@@ -114,6 +114,20 @@ def test_test_world(rtx, oracle):
     np.testing.assert_array_equal(v, w.mat_values)
 
 
+def test_ps_world(rtx):
+    """Shader_RT.fx:300-335: ground, three small Lambert spheres, glass, Lambert, metal."""
+    w = rtx.ps_world()
+    assert (w.count, w.depth, w.spp) == (7, 25, 1)
+    np.testing.assert_array_equal(w.spheres, np.array([
+        [0, -1000, 0, 1000], [3, 0.2, 1.5, 0.2], [4.5, 0.2, 1, 0.2], [4.5, 0.2, 2, 0.2],
+        [0, 1, 0, 1], [-4, 1, 0, 1], [4, 1, 0, 1]], np.float32))
+    np.testing.assert_array_equal(w.mat_types, [0, 0, 0, 0, 2, 0, 1])
+    np.testing.assert_array_equal(w.mat_values[:, :3], np.array([
+        [0.5, 0.5, 0.5], [0.2, 0.2, 0.8], [0.2, 0.8, 0.2], [0.8, 0.3, 0.2],
+        [1, 1, 1], [0.4, 0.2, 0.1], [0.7, 0.6, 0.5]], np.float32))
+    assert w.mat_values[4, 3] == np.float32(1.5) and w.mat_values[6, 3] == 0.0
+
+
 def test_camera_kat(rtx, oracle):
     """PerFrame::ComputeViewVals for camPos (13,2,3) -> 0, vfov 20, 16:9 (DxCSApp.cpp:39-61, 176-179)."""
     f = rtx.camera_look_at(1024, 576)

@@ -107,6 +107,44 @@ def test_oracle_row_order_and_threads_invariant(oracle, rtx):
     assert sa == sb
 
 
+def lambert_cases(n=4000, seed=5):
+    """Random (p, normal, rius) plus engineered zero directions: at |p| = 1000
+    the fp32 sums ((p + n) + rius) - p cancel to exactly 0 when rius ~ -n."""
+    rng = np.random.default_rng(seed)
+    p = rng.uniform(-20, 20, (n, 3)).astype(np.float32)
+    nrm = rng.normal(size=(n, 3))
+    nrm = (nrm / np.linalg.norm(nrm, axis=1, keepdims=True)).astype(np.float32)
+    rius = rng.uniform(-0.5, 0.5, (n, 3)).astype(np.float32)
+    zp = np.array([[0, 1000, 0], [1000, 0, 0], [0, 0, -1000], [512, -512, 1024]], np.float32)
+    zn = np.array([[0, 1, 0], [1, 0, 0], [0, 0, -1], [0, -1, 0]], np.float32)
+    zr = -zn * np.float32(0.99999994)
+    return np.concatenate([p, zp]), np.concatenate([nrm, zn]), np.concatenate([rius, zr]), len(zp)
+
+
+def test_lambert_guard_oracle(oracle):
+    """f-4: without the guard a zero diffuse direction normalises to NaN (the
+    compute shader, ShaderCompute.hlsl:211-212); with it, to the normal
+    (Shader_RT.fx:222-225, near_zero of ShaderCompute.hlsl:70-74)."""
+    p, nrm, rius, nz = lambert_cases()
+    plain = oracle.lambert_dir(p, nrm, rius, guard=False)
+    guard = oracle.lambert_dir(p, nrm, rius, guard=True)
+    np.testing.assert_array_equal(plain[:-nz].view(np.uint32), guard[:-nz].view(np.uint32))
+    assert np.isnan(plain[-nz:]).all()
+    np.testing.assert_array_equal(guard[-nz:], nrm[-nz:])
+
+
+def test_lambert_guard_frame_flag(oracle, rtx):
+    """On ordinary frames the guard never fires: the same image bit for bit."""
+    world = rtx.ps_world(depth=25, spp=2)
+    f0 = rtx.camera_look_at(48, 27, aspect=48 / 27)
+    f1 = rtx.camera_look_at(48, 27, aspect=48 / 27)
+    f1.flags = rtx.FRAME_LAMBERT_GUARD
+    a, sa = oracle.render_rows(world, f0, np.arange(27))
+    b, sb = oracle.render_rows(world, f1, np.arange(27))
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa == sb
+
+
 def test_thin_lens_changes_only_when_enabled(oracle, rtx):
     world = rtx.random_world(4, depth=10, spp=2)
     pin = rtx.camera_look_at(32, 18, aspect=32 / 18)
