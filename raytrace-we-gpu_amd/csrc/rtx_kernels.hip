@@ -83,6 +83,9 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
 #define RTX_DIAG_PROF 0
 #endif
+#ifndef RTX_LPT_DEAL  // 1: deal the initial fill of the normal queue round-robin over the waves
+#define RTX_LPT_DEAL 0
+#endif
 #ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
 #define RTX_DIAG_PIXEL 0
 #endif
@@ -129,7 +132,7 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #define RTX_HEAVY_RHO 1.2
 #endif
 #ifndef RTX_HEAVY1_ALPHA  // tier 1 iff key > alpha1 * a lane's share of the summed keys
-#define RTX_HEAVY1_ALPHA 2.0
+#define RTX_HEAVY1_ALPHA 1.7
 #endif
 #ifndef RTX_HEAVY1_ALPHA_SMALL  // the same for a small frame share
 #define RTX_HEAVY1_ALPHA_SMALL 4.0
@@ -485,10 +488,32 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
 // disc < 0) is skipped, like the reference's `if (d < 0) return false`.
 // Returns false if a candidate has a non-finite root (the lane then takes
 // hit_blocks_seq).
-__device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint32_t n, const uint32_t *list,
-                                            uint32_t m, f3 o, f3 d, float a, float inv_a, float t_min,
-                                            float &best, int &idx) {
+// One candidate: sc = (center, radius) of sphere g; live = it is one.
+__device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f3 d, float a, float inv_a,
+                                            float t_min, float &best, int &idx, bool &ok) {
     const float inf = __uint_as_float(0x7f800000u);
+    const float ocx = o.x - sc.x;
+    const float ocy = o.y - sc.y;
+    const float ocz = o.z - sc.z;
+    const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+    const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(sc.w * sc.w))));
+    const float disc = fmaf(hb, hb, -(a * cc));
+    const bool cand = live && !(disc < 0.0f);
+    const float sq = sqrtf(disc);
+    const float rn = (-hb - sq) * inv_a;
+    const float rf = (-hb + sq) * inv_a;
+    ok = ok && !(cand && !(fabsf(rn) < inf && fabsf(rf) < inf));
+    const bool use_n = !(rn < t_min);
+    const float c = use_n ? rn : rf;
+    const bool acc = cand && (use_n || !(rf < t_min)) && (c < best || (c == best && g > idx));
+    best = acc ? c : best;
+    idx = acc ? g : idx;
+}
+
+// `ld(i)` returns (center, radius) of sphere i < n.
+template <typename Ld>
+__device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t *list, uint32_t m, f3 o, f3 d,
+                                              float a, float inv_a, float t_min, float &best, int &idx) {
     bool ok = true;
     uint32_t j = 0;
     uint32_t e = list[threadIdx.x];  // entry 0 (unused when m == 0)
@@ -502,26 +527,14 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
         j += adv ? 1u : 0u;
         const uint32_t nx = list[min(j, (uint32_t)kCand) * kRB + threadIdx.x];
         e = adv ? nx : e;
-        const float4 sc = cen[min(i, n - 1u)];
-        const float ocx = o.x - sc.x;
-        const float ocy = o.y - sc.y;
-        const float ocz = o.z - sc.z;
-        const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(sc.w * sc.w))));
-        const float disc = fmaf(hb, hb, -(a * cc));
-        const bool cand = live && !(disc < 0.0f);
-        const float sq = sqrtf(disc);
-        const float rn = (-hb - sq) * inv_a;
-        const float rf = (-hb + sq) * inv_a;
-        ok = ok && !(cand && !(fabsf(rn) < inf && fabsf(rf) < inf));
-        const bool use_n = !(rn < t_min);
-        const float c = use_n ? rn : rf;
-        const int g = (int)i;
-        const bool acc = cand && (use_n || !(rf < t_min)) && (c < best || (c == best && g > idx));
-        best = acc ? c : best;
-        idx = acc ? g : idx;
+        resolve_one(ld(min(i, n - 1u)), (int)i, live, o, d, a, inv_a, t_min, best, idx, ok);
     }
     return ok;
+}
+__device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint32_t n, const uint32_t *list,
+                                            uint32_t m, f3 o, f3 d, float a, float inv_a, float t_min,
+                                            float &best, int &idx) {
+    return resolve_pre_t([cen](uint32_t i) { return cen[i]; }, n, list, m, o, d, a, inv_a, t_min, best, idx);
 }
 
 // hit_world with the prefiltered scan: same (best, idx) as the in-order
@@ -580,27 +593,54 @@ constexpr uint32_t kCoopBytes = (kRB / 64) * kCoopWaveBytes;
 #define RTX_COOP_STEP 2
 #endif
 constexpr uint32_t kCoopStep = RTX_COOP_STEP;  // spheres per coop step (reads in flight)
-constexpr uint32_t kCoopLds = 768;  // scenes up to this many spheres keep pre4 in LDS for the coop (12 KiB)
+constexpr uint32_t kCoopLds = 704;  // scenes up to this many spheres keep pre4 + radii in LDS for the coop (<= 13.75 KiB: 5 blocks/CU)
 static_assert(RTX_COOP_MAX <= (int)kCoopSlots, "RTX_COOP_MAX must be <= 32");
 
-template <typename Q4>
-__device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64_t act, bool active, f3 o,
-                                                f3 d, float a, float inv_a, float t_min, float *ws,
-                                                uint32_t *list, float &best, bool &seq,
-                                                unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
+// Reduction over aligned groups of 2^lg lanes (lg wave-uniform, whole wave
+// active): DPP inside a row of 16 (quad_perm xor 1 and xor 2, then the
+// half-row and row mirrors, which pair each lane with one in the other half),
+// ds_swizzle xor 16, ds_bpermute xor 32. Every lane of a group ends with the
+// group's min (or max).
+template <bool kMax>
+__device__ __forceinline__ uint32_t group_reduce_u32(uint32_t v, uint32_t lg) {
+    auto op = [](uint32_t x, uint32_t y) { return kMax ? max(x, y) : min(x, y); };
+    if (lg >= 1u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    if (lg >= 2u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    if (lg >= 3u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    if (lg >= 4u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+    if (lg >= 5u) v = op(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F));
+    if (lg >= 6u) v = op(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+    return v;
+}
+
+__device__ __forceinline__ float read_lane(float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+// (Reading the tier-1 ray itself with readlane instead of through LDS costs
+// 4 VGPRs in this kernel: 98, one wave per SIMD less.)
+
+// Rays go through the wave's LDS slot; results too, except for kOne (a
+// single ray, tier 1): its line is then kept in scalars and its result,
+// left in every lane by the reduction, is read directly. rad != nullptr: sph4 and rad are the block's LDS copies
+// (resolve reads them instead of S.cen).
 #define RTX_CP(k)                                                   \
     if (RTX_DIAG_COOP && cp) {                                      \
         const unsigned long long tn = __builtin_readcyclecounter(); \
         cp[k] += tn - *tq;                                          \
         *tq = tn;                                                   \
     }
+template <bool kOne, typename Q4>
+__device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,
+                                           f3 o, f3 d, float a, float inv_a, float t_min, float *ws,
+                                           uint32_t *list, float &best, bool &seq, unsigned long long *cp,
+                                           unsigned long long *tq) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t m = (uint32_t)__popcll(act);
+    const uint32_t m = kOne ? 1u : (uint32_t)__popcll(act);
     const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
     const uint32_t g = 1u << lg;
-    const uint32_t rank =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    uint32_t rank;
     uint32_t *keys = reinterpret_cast<uint32_t *>(ws + 8 * kCoopSlots);
+    rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     if (active) {
         float *w = ws + 8 * rank;
         w[0] = o.x;
@@ -615,8 +655,19 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
     __builtin_amdgcn_wave_barrier();
     const uint32_t r = lane >> lg, k = lane & (g - 1u);
     const bool valid = r < m;
-    const float *w = ws + 8 * (valid ? r : 0u);  // the group's ray (re-read where needed: fewer live VGPRs)
-    const LineTest T = line_test_setup(w[0], w[1], w[2], w[3], w[4], w[5], w[6], S.smag);
+    // the group's ray (LDS: re-read where needed, fewer live VGPRs)
+    const float *w = ws + 8 * (valid ? r : 0u);
+    LineTest T = line_test_setup(w[0], w[1], w[2], w[3], w[4], w[5], w[6], S.smag);
+    if constexpr (kOne) {  // uniform: keep the line in SGPRs
+        T.ux = read_lane(T.ux, 0);
+        T.uz = read_lane(T.uz, 0);
+        T.vx = read_lane(T.vx, 0);
+        T.vy = read_lane(T.vy, 0);
+        T.vz = read_lane(T.vz, 0);
+        T.nou = read_lane(T.nou, 0);
+        T.nov = read_lane(T.nov, 0);
+        T.thr = read_lane(T.thr, 0);
+    }
     RTX_CP(0)
     const uint32_t n = S.n;
     // lane k of a group scans the contiguous chunk [k*ch, k*ch + ch) of the
@@ -629,7 +680,30 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
     float bc = __uint_as_float(0x7f800000u);
     int bg = -1;
     bool ok = true;
-    do {
+    if constexpr (kOne) {
+        // one ray: a flagged sphere is resolved on the spot (a handful per
+        // ray), no candidate list
+        const f3 ro = mk3(read_lane(w[0], 0), read_lane(w[1], 0), read_lane(w[2], 0));
+        const f3 rd = mk3(read_lane(w[3], 0), read_lane(w[4], 0), read_lane(w[5], 0));
+        const float ra = read_lane(w[6], 0), ria = read_lane(w[7], 0);
+        for (;;) {
+            const bool more = i < i1;
+            if (__ballot(more) == 0ull) break;
+            float4 pq[kCoopStep];
+#pragma unroll
+            for (uint32_t u = 0; u < kCoopStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
+#pragma unroll
+            for (uint32_t u = 0; u < kCoopStep; ++u) {
+                const uint32_t j = i + u;
+                if (j < i1 && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr)) {
+                    const float rr = rad ? rad[j] : S.cen[j].w;
+                    resolve_one(make_float4(pq[u].x, pq[u].y, pq[u].z, rr), (int)j, true, ro, rd, ra, ria, t_min,
+                                bc, bg, ok);
+                }
+            }
+            i = more ? i + kCoopStep : i;
+        }
+    } else do {
         uint32_t cnt = 0;
         for (;;) {
             const bool more = i < i1;
@@ -648,40 +722,73 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, uint64
             i = more ? i + kCoopStep : i;
             if (__ballot(cnt == (uint32_t)kCand) != 0ull) break;
         }
-        ok = resolve_pre(S.cen, n, list, cnt, mk3(w[0], w[1], w[2]), mk3(w[3], w[4], w[5]), w[6], w[7], t_min,
-                         bc, bg) && ok;
+        const f3 ro = mk3(w[0], w[1], w[2]), rd = mk3(w[3], w[4], w[5]);
+        if (rad)
+            ok = resolve_pre_t(
+                     [sph4, rad](uint32_t j) {
+                         const float4 q = sph4[j];
+                         return make_float4(q.x, q.y, q.z, rad[j]);
+                     },
+                     n, list, cnt, ro, rd, w[6], w[7], t_min, bc, bg) &&
+                 ok;
+        else
+            ok = resolve_pre(S.cen, n, list, cnt, ro, rd, w[6], w[7], t_min, bc, bg) && ok;
     } while (__ballot(i < i1) != 0ull);
     RTX_CP(1)
-    // c >= t_min > 0: its bits order like its value; ties -> larger index
-    uint64_t key = bg >= 0 ? ((uint64_t)__float_as_uint(bc) << 32) | (uint64_t)(0xffffffffu - (uint32_t)bg)
-                           : ~0ull;
-    for (uint32_t sh = g >> 1; sh != 0u; sh >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, (int)sh, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), (int)sh, 64);
-        const uint64_t other = ((uint64_t)hi << 32) | lo;
-        key = other < key ? other : key;
-    }
+    // the group's (min c, then the largest index among equal c): the rule of
+    // the in-order scan. c >= t_min > 0, so its bits order like its value.
+    const uint32_t cb0 = bg >= 0 ? __float_as_uint(bc) : 0x7f800000u;
+    const uint32_t cb = group_reduce_u32<false>(cb0, lg);
+    const uint32_t ib = group_reduce_u32<true>(bg >= 0 && cb0 == cb ? (uint32_t)bg + 1u : 0u, lg);
     const uint64_t badm = __ballot(!ok);
-    if (valid && k == 0u) {
-        const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
-        const uint64_t out = (badm & gm) != 0ull ? 0ull : key;  // 0: a non-finite root in the group
-        keys[2 * r] = (uint32_t)out;
-        keys[2 * r + 1] = (uint32_t)(out >> 32);
-    }
-    __builtin_amdgcn_wave_barrier();
-    RTX_CP(2)
     seq = false;
-    if (!active) return -1;
-    const uint64_t kk = ((uint64_t)keys[2 * rank + 1] << 32) | keys[2 * rank];
-    if (kk == 0ull) {
-        seq = true;
-        return -1;
+    if constexpr (kOne) {
+        RTX_CP(2)
+        if (!active) return -1;
+        if (badm != 0ull) {  // a non-finite root: the exact sequential path
+            seq = true;
+            return -1;
+        }
+        if (ib == 0u) return -1;
+        const float c = __uint_as_float(cb);
+        if (!(c <= best)) return -1;  // accepted iff c <= t_max
+        best = c;
+        return (int)(ib - 1u);
+    } else {
+        if (valid && k == 0u) {
+            const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
+            // 0: a non-finite root in the group; ~0: no hit
+            const uint64_t out = (badm & gm) != 0ull ? 0ull
+                                 : ib == 0u      ? ~0ull
+                                                 : ((uint64_t)cb << 32) | (uint64_t)(0xffffffffu - (ib - 1u));
+            keys[2 * r] = (uint32_t)out;
+            keys[2 * r + 1] = (uint32_t)(out >> 32);
+        }
+        __builtin_amdgcn_wave_barrier();
+        RTX_CP(2)
+        if (!active) return -1;
+        const uint64_t kk = ((uint64_t)keys[2 * rank + 1] << 32) | keys[2 * rank];
+        if (kk == 0ull) {
+            seq = true;
+            return -1;
+        }
+        if (kk == ~0ull) return -1;
+        const float c = __uint_as_float((uint32_t)(kk >> 32));
+        if (!(c <= best)) return -1;
+        best = c;
+        return (int)(0xffffffffu - (uint32_t)kk);
     }
-    if (kk == ~0ull) return -1;
-    const float c = __uint_as_float((uint32_t)(kk >> 32));
-    if (!(c <= best)) return -1;  // accepted iff c <= t_max
-    best = c;
-    return (int)(0xffffffffu - (uint32_t)kk);
+}
+#undef RTX_CP
+
+template <typename Q4>
+__device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, const float *rad, uint64_t act,
+                                                bool active, f3 o, f3 d, float a, float inv_a, float t_min,
+                                                float *ws, uint32_t *list, float &best, bool &seq,
+                                                unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
+    if (__popcll(act) == 1)
+        return groups_impl<true>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
+    return groups_impl<false>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
 }
 
 // Lane state: the pixel it is tracing and that pixel's current path.
@@ -917,6 +1024,11 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // segment); tier 2 = slots [k1, kh), up to kHeavy2 per wave. An idle wave
 // tries tier 1 first; a tier-2 wave tops itself up from tier 2. Returns the
 // wave's tier (0: not heavy any more).
+// Cost rank of normal-queue slot `slot` (inverse of deal_slot).
+__device__ __forceinline__ uint32_t slot_rank(uint32_t slot, uint32_t kh, uint32_t w) {
+    const uint32_t q = slot - kh;  // slot >= kh for normal-queue pixels
+    return q < w * 64u ? (q & 63u) * w + (q >> 6) : q;
+}
 constexpr uint32_t kHeavy1 = RTX_HEAVY1_WAVE;
 constexpr uint32_t kHeavy2 = RTX_HEAVY_WAVE;
 struct HeavyState {
@@ -974,9 +1086,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #if RTX_SRC == 1
     // the coop's sphere data: a block-wide LDS copy of pre4 for small scenes
     float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kListBytes + kCoopBytes);
+    float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
     const bool coop_lds = P.scene.n <= kCoopLds;
     if (coop_lds) {
-        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) s_pre4[i] = P.scene.pre4[i];
+        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
+            s_pre4[i] = P.scene.pre4[i];
+            s_rad[i] = P.scene.cen[i].w;
+        }
         __syncthreads();
     }
 #endif
@@ -1009,6 +1125,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
+    // waves the initial fill was dealt over (k_cost_scatter), for slot_rank
+    const uint32_t deal_w = RTX_LPT_DEAL && kPersist && P.perm ? min(gridDim.x * kRB, npix - kh) / 64u : 0u;
 #if RTX_DIAG_PROF
     // [0] refill clocks [1] hit_world [2] shade [3] tail mode [4] iterations [5] tail iterations
     // [6] active lanes summed over iterations
@@ -1072,10 +1190,12 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #else
             unsigned long long *cp = nullptr, *ctqp = nullptr;
 #endif
-            int my_hit = coop_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, act, L.active, L.o, L.d, L.a,
-                                                     L.inv_a, kTMin, coop_ws, list, my_best, my_seq, cp, ctqp)
-                                  : hit_world_groups(P.scene, P.scene.pre4, act, L.active, L.o, L.d, L.a, L.inv_a,
-                                                     kTMin, coop_ws, list, my_best, my_seq, cp, ctqp);
+            int my_hit = coop_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, (const float *)s_rad, act,
+                                                     L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list,
+                                                     my_best, my_seq, cp, ctqp)
+                                  : hit_world_groups(P.scene, P.scene.pre4, (const float *)nullptr, act, L.active,
+                                                     L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list, my_best, my_seq,
+                                                     cp, ctqp);
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
@@ -1091,7 +1211,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             }
             was_t1 = H.tier == 1u;
 #endif
-            __builtin_amdgcn_s_setprio(0);
+            if (H.tier == 0u) __builtin_amdgcn_s_setprio(0);  // a heavy wave keeps its priority
             RTX_PROF(3)
             continue;
         }
@@ -1100,7 +1220,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
-        if (__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull)
+        if (__ballot(L.active && slot_rank(L.slot, kh, deal_w) < P.prio_slots) != 0ull)
             __builtin_amdgcn_s_setprio(3);
         else
             __builtin_amdgcn_s_setprio(0);
@@ -1191,6 +1311,9 @@ __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, u
         }
     }
     sum += RTX_LPT_CW * cost[i];
+    // scaled to 9 one-sample costs (the 3x3, 1-spp key the tiers were tuned on)
+    constexpr uint32_t kWin = (2 * RTX_LPT_RADIUS + 1) * (2 * RTX_LPT_RADIUS + 1) * kCostSpp;
+    if (kWin != 9u) sum = (sum * 9u + kWin / 2u) / kWin;
     return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
 }
 constexpr uint32_t kSortPerThread = 16;
@@ -1214,9 +1337,21 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // Positions: bucket start (prefix of the global counts) + a range the
 // block reserves in the bucket + the element's rank inside the block. The
 // order within a bucket is arbitrary; per-pixel results do not depend on it.
+// The first `fill` slots of the normal queue (after the kh heavy slots,
+// heavy[1]) are dealt round-robin over the waves of the initial fill: wave
+// w's 64 slots get ranks w, w + W, w + 2W, ... (W = fill / 64), so the
+// costliest lane-mode pixels are spread one per wave instead of packed into
+// the first waves (which share CUs and would fight over the same SIMDs).
+__device__ __forceinline__ uint32_t deal_slot(uint32_t pos, uint32_t kh, uint32_t nn) {
+    if (pos < kh) return pos;
+    const uint32_t q = pos - kh;
+    const uint32_t w = nn / 64u;  // waves dealt (whole ones)
+    if (q >= w * 64u) return pos;
+    return kh + (q % w) * 64u + q / w;
+}
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          const uint32_t *counts, uint32_t *cursors,
-                                                         uint32_t *perm) {
+                                                         uint32_t *perm, const uint32_t *heavy, uint32_t fill) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -1240,9 +1375,11 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
+    const uint32_t kh = heavy ? min(heavy[1], n) : 0u;
+    const uint32_t nn = min(fill, n - kh);
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) perm[start[key[k]] + rank[k]] = i;
+        if (i < n) perm[deal_slot(start[key[k]] + rank[k], kh, RTX_LPT_DEAL ? nn : 0u)] = i;
     }
 }
 
@@ -1394,7 +1531,7 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
     if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
-    const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * sizeof(float4) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
+    const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
     hipError_t e = allow_lds((const void *)k_render<false>, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render<false>, dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
@@ -1411,7 +1548,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     }
     hipError_t e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
-        const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * sizeof(float4) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
+        const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
         e = allow_lds((const void *)k_render<true>, lds);
         if (e == hipSuccess) e = allow_lds((const void *)k_render<false>, lds);
         if (e != hipSuccess) return e;
@@ -1435,15 +1572,19 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
         hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                            p.rows_local, sched.buckets);
-        hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
-        // 3. heavy-pixel split, then the persistent render over the ordered queue
+        // 3. heavy-pixel split (from the histogram), the ordered queue, then
+        // the persistent render over it
         const uint32_t blocks = min(need, resident_blocks((const void *)k_render<true>, lds));
         uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
         hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
+        hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
+                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
+                           (const uint32_t *)(RTX_HEAVY_WAVE ? heavy : nullptr), blocks * kRB);
         KParams q = p;
         q.perm = sched.perm;
-        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u);
+        // the top ranks of the normal queue run at top priority: with the
+        // deal, ranks < W are lane 0 of every wave, so a fraction of W
+        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u / (RTX_LPT_DEAL ? 64u : 1u));
         q.heavy = RTX_HEAVY_WAVE ? heavy : nullptr;
         e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;

@@ -41,7 +41,7 @@ for s in $STEPS; do
     sprof)  run sprof 300 python tools/section_prof.py raytrace-we-gpu_amd/lib/variants/librtx_prof.so ;;
     parts)  run parts 600 python tools/part_scaling.py ${PLIBS:-} ;;
     cprof)  run cprof 300 python tools/coop_prof.py raytrace-we-gpu_amd/lib/variants/librtx_cprof.so ;;
-    ptime)  run ptime 600 python tools/pixel_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_ptime.so \
+    ptime)  run ptime 600 python tools/pixel_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_${PTLIB:-ptime}.so \
                 --parts ${PTPARTS:-1 2 8} ;;
     cost)   run cost 600 python tools/cost_analysis.py --out "$OUT/cost.npz" ;;
     c5)     run c5 900 python tools/variant_bench.py --rounds 2 --frames 1 --spp 16 --grid 159 --max-spheres 100000 ${C5V:-} ;;
