@@ -45,14 +45,11 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof c16 c32 c16p2
+VARIANTS := best prof ptime cprof
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
-VFLAGS_c16           := -DRTX_COOP_MAX=16
-VFLAGS_c32           := -DRTX_COOP_MAX=32
-VFLAGS_c16p2         := -DRTX_COOP_MAX=16 -DRTX_TAIL_PRIO=2
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
