@@ -313,6 +313,10 @@ uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part, uint3
 static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
                        float4 *accum, uint32_t accum_frames, uint32_t frame_index);
 
+// Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + 4], then the
+// per-pixel pre-pass state (float4, 16-byte aligned).
+static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 4 + 3) & ~(size_t)3; }
+
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
     return render_impl(c, tile_rows, part, nparts, d_out, nullptr, 0, c->frame.frame_index);
@@ -420,13 +424,15 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         (void)hipFree(c->d_sched);
         c->d_sched = nullptr;
         c->sched_pixels = 0;
-        RTX_HIP(hipMalloc(&c->d_sched, (2 * npix + 2 * rtx::kCostBuckets + 4) * sizeof(uint32_t)));
+        // cost, perm, buckets; then 16-byte aligned per-pixel state
+        RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix) * sizeof(uint32_t)));
         c->sched_pixels = npix;
     }
     rtx::KSchedule sched;
     sched.cost = c->d_sched;
     sched.perm = c->d_sched + c->sched_pixels;
     sched.buckets = c->d_sched + 2 * c->sched_pixels;
+    sched.state = reinterpret_cast<float4 *>(c->d_sched + sched_state_off(c->sched_pixels));
     sched.npix = (uint32_t)c->sched_pixels;
     sched.nbuckets = rtx::kCostBuckets;
     hipError_t e = rtx::launch_render(p, sched, c->stream);

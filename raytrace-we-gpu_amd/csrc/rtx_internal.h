@@ -57,6 +57,8 @@ struct KParams {
     uint32_t wave_cap;             // pairs in wave_times
     const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
+    float4 *state;                 // per pixel (acc, seed) after kCostSpp samples: written by the
+                                   // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
 };
@@ -69,6 +71,7 @@ struct KParams {
 struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
+    float4 *state;      // [npix] (acc.xyz, seed) after the pre-pass's samples
     uint32_t *buckets;  // [2 * nbuckets + 4]: counts, cursors, heavy counters and ends (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object

@@ -834,6 +834,8 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
     if (P.cost_out) {  // scheduling pre-pass: one pixel per lane, record its segments
         P.cost_out[L.gid] = L.segs;
+        // and its state after these samples: the render resumes from it
+        if (P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
         return;
     }
     // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
@@ -981,9 +983,16 @@ __device__ __forceinline__ Frame load_frame(const KParams &P) {
 __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, uint32_t gid, Lane &L) {
     L.gid = gid;
     lane_pixel(P, gid, L.x, L.y);
-    L.acc = mk3(0.0f, 0.0f, 0.0f);
-    L.sample = 0;
-    L.seed = pixel_seed(P, L.x, L.y, 0);
+    if (P.state && !P.cost_out) {  // after the pre-pass's kCostSpp samples (identical state)
+        const float4 st = P.state[gid];
+        L.acc = mk3(st.x, st.y, st.z);
+        L.sample = kCostSpp;
+        L.seed = st.w;
+    } else {
+        L.acc = mk3(0.0f, 0.0f, 0.0f);
+        L.sample = 0;
+        L.seed = pixel_seed(P, L.x, L.y, 0);
+    }
     L.active = true;
     begin_sample(P, F, L.x, L.y, L);
 }
@@ -1297,6 +1306,9 @@ __global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
 #ifndef RTX_LPT_RADIUS
 #define RTX_LPT_RADIUS 1
 #endif
+#ifndef RTX_LPT_RESUME  // 1: the render resumes each pixel after the pre-pass's samples
+#define RTX_LPT_RESUME 1
+#endif
 #ifndef RTX_LPT_CW  // extra weight of the centre pixel
 #define RTX_LPT_CW 0
 #endif
@@ -1561,8 +1573,9 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         KParams c = p;
         c.spp = min(p.spp, kCostSpp);
         c.cost_out = sched.cost;
+        c.state = RTX_LPT_RESUME ? sched.state : nullptr;  // the first kCostSpp samples, not traced again
+        if (!RTX_LPT_RESUME) c.counters = p.counters + 3;     // scratch: not part of the frame's count
         c.accum = nullptr;
-        c.counters = p.counters + 3;  // scratch: not part of the frame's segment count
         c.wave_times = nullptr;
         c.perm = nullptr;
         e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
@@ -1582,6 +1595,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
                            (const uint32_t *)(RTX_HEAVY_WAVE ? heavy : nullptr), blocks * kRB);
         KParams q = p;
         q.perm = sched.perm;
+        q.state = RTX_LPT_RESUME ? sched.state : nullptr;
         // the top ranks of the normal queue run at top priority: with the
         // deal, ranks < W are lane 0 of every wave, so a fraction of W
         q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u / (RTX_LPT_DEAL ? 64u : 1u));
