@@ -798,6 +798,7 @@ struct Lane {
     uint32_t sample, bounce, segs;
     uint32_t x, y, gid;  // pixel (global image coords) and its output slot
     uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
+    uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments)
     bool active;         // tracing a pixel
 };
 
@@ -831,9 +832,10 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 // Shading of one finished hit_world call (sample_color body, :262-284, and
 // scatter, :207-252). Advances the lane to its next sample when the path
 // ends; clears `active` after the pixel's last sample.
+template <bool kCost = false>
 __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
-    if (P.cost_out) {  // scheduling pre-pass: one pixel per lane, record its segments
-        P.cost_out[L.gid] = L.segs;
+    if constexpr (kCost) {  // scheduling pre-pass: record the pixel's segments
+        P.cost_out[L.gid] = L.segs - L.seg0;
         // and its state after these samples: the render resumes from it
         if (P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
         return;
@@ -868,6 +870,7 @@ __device__ __forceinline__ f3 lambert_guard(f3 v, f3 nrm, bool guard) {
     return guard && nz ? nrm : v;
 }
 
+template <bool kCost = false>
 __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
     L.segs++;
     bool ended = false;
@@ -938,7 +941,7 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
     if (ended) {
         L.sample++;
         if (L.sample >= P.spp) {
-            write_pixel(P, L);
+            write_pixel<kCost>(P, L);
             L.active = false;
 #if RTX_DIAG_PIXEL
             if (P.wave_times && L.gid < P.wave_cap) P.wave_times[2 * L.gid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -983,6 +986,7 @@ __device__ __forceinline__ Frame load_frame(const KParams &P) {
 __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, uint32_t gid, Lane &L) {
     L.gid = gid;
     lane_pixel(P, gid, L.x, L.y);
+    L.seg0 = L.segs;
     if (P.state && !P.cost_out) {  // after the pre-pass's kCostSpp samples (identical state)
         const float4 st = P.state[gid];
         L.acc = mk3(st.x, st.y, st.z);
@@ -1084,8 +1088,9 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // resident in LDS (one copy per workgroup), 1 reads them with scalar loads.
 // kPersist: the grid holds as many waves as the GPU keeps resident and
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
-// otherwise an exact grid, one pixel per lane.
-template <bool kPersist>
+// otherwise an exact grid, one pixel per lane. kCost: the scheduling
+// pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
+template <bool kPersist, bool kCost = false>
 __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     // dynamic LDS: [candidate list, kListBytes][coop rays, kCoopBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -1210,7 +1215,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                     my_best = __uint_as_float(0x7f800000u);
                     my_hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
-                shade(P, F, L, min(my_hit, last), my_best);
+                shade<kCost>(P, F, L, min(my_hit, last), my_best);
             }
 #if RTX_DIAG_COOP
             if (cp) {
@@ -1242,7 +1247,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             const int hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
 #endif
             RTX_PROF(1)
-            shade(P, F, L, min(hit, last), best);
+            shade<kCost>(P, F, L, min(hit, last), best);
         }
         RTX_PROF(2)
     }
@@ -1305,6 +1310,9 @@ __global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
 // at the edges), which averages that noise over similar pixels.
 #ifndef RTX_LPT_RADIUS
 #define RTX_LPT_RADIUS 1
+#endif
+#ifndef RTX_LPT_PERSIST_PREPASS  // 1: the cost pre-pass runs on persistent lanes (index order; measured ~1 % slower)
+#define RTX_LPT_PERSIST_PREPASS 0
 #endif
 #ifndef RTX_LPT_RESUME  // 1: the render resumes each pixel after the pre-pass's samples
 #define RTX_LPT_RESUME 1
@@ -1544,9 +1552,9 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
     if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
     const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
-    hipError_t e = allow_lds((const void *)k_render<false>, lds);
+    hipError_t e = allow_lds((const void *)k_render<false, true>, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_render<false>, dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
+    hipLaunchKernelGGL((k_render<false, true>), dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -1563,6 +1571,8 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
         e = allow_lds((const void *)k_render<true>, lds);
         if (e == hipSuccess) e = allow_lds((const void *)k_render<false>, lds);
+        if (e == hipSuccess) e = allow_lds((const void *)k_render<true, true>, lds);
+        if (e == hipSuccess) e = allow_lds((const void *)k_render<false, true>, lds);
         if (e != hipSuccess) return e;
         if (!RTX_PERSISTENT || !sched.cost || p.spp < kLptMinSpp) {
             hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, p);
@@ -1577,10 +1587,20 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         if (!RTX_LPT_RESUME) c.counters = p.counters + 3;     // scratch: not part of the frame's count
         c.accum = nullptr;
         c.wave_times = nullptr;
-        c.perm = nullptr;
+        c.perm = nullptr;  // index order
+        c.heavy = nullptr;
+        c.prio_slots = 0;
         e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, c);
+#if RTX_LPT_PERSIST_PREPASS
+        // persistent lanes: a lane whose pixel ends takes the next one, so the
+        // pass does not wait on each wave's slowest pixel
+        const uint32_t cblocks = min(need, resident_blocks((const void *)k_render<true, true>, lds));
+        hipLaunchKernelGGL((k_render<true, true>), dim3(cblocks), dim3(kRB), lds, stream, c);
+#else
+        hipLaunchKernelGGL((k_render<false, true>), dim3(need), dim3(kRB), lds, stream, c);
+#endif
         // 2. counting sort by cost, descending
         const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
         hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
