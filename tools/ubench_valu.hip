@@ -38,6 +38,23 @@ __global__ void __launch_bounds__(256) k_pkfma(float *out, int iters, float a, f
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+template <int CHAINS>
+__global__ void __launch_bounds__(256) k_pkfma16(float *out, int iters, float a, float b) {
+    half2v acc[CHAINS];
+    const half2v av = {(_Float16)a, (_Float16)a}, bv = {(_Float16)b, (_Float16)b};
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) acc[c] = (half2v){(_Float16)(threadIdx.x * 1e-3f + c), (_Float16)(c * 0.5f)};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) acc[c] = __builtin_elementwise_fma(acc[c], av, bv);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) s += (float)acc[c].x + (float)acc[c].y;
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 int main() {
     hipDeviceProp_t p;
     (void)hipGetDeviceProperties(&p, 0);
@@ -64,6 +81,13 @@ int main() {
         (void)hipEventElapsedTime(&ms, e0, e1);
         const double fl2 = 2.0 * 16 * iters * (double)blocks * 256;
         std::printf("{\"kernel\": \"v_pk_fma_f32 x8 chains\", \"cus\": %d, \"ms\": %.3f, \"tflops\": %.2f}\n",
+                    p.multiProcessorCount, ms, fl2 / ms / 1e9);
+        (void)hipEventRecord(e0);
+        hipLaunchKernelGGL(k_pkfma16<8>, dim3(blocks), dim3(256), 0, 0, out, iters, 0.999f, 0.001f);
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        std::printf("{\"kernel\": \"v_pk_fma_f16 x8 chains\", \"cus\": %d, \"ms\": %.3f, \"tflops\": %.2f}\n",
                     p.multiProcessorCount, ms, fl2 / ms / 1e9);
     }
     (void)hipFree(out);
