@@ -383,6 +383,27 @@ def test_thin_lens_bit_exact(gpu_ctx, oracle, rtx):
     assert st.segments == segs
 
 
+@pytest.mark.parametrize("mode", ["chain", "per_sample_rng", "thin_lens", "frame_index", "lambert_guard"])
+def test_scheduled_path_with_frame_options(gpu_ctx, oracle, rtx, mode):
+    """spp >= 8 takes the cost pre-pass + ordered persistent render, which
+    resumes every pixel after the pre-pass's sample 0 (acc, seed); each frame
+    option must survive that hand-off bit for bit."""
+    world = rtx.random_world(11, depth=50, spp=10)
+    frame = rtx.camera_look_at(160, 90, aspect=160 / 90)
+    if mode == "per_sample_rng":
+        frame.rng_mode = 1
+    elif mode == "thin_lens":
+        frame = rtx.set_aperture(frame, 0.4)
+    elif mode == "frame_index":
+        frame.frame_index = 3
+    elif mode == "lambert_guard":
+        frame.flags = rtx.FRAME_LAMBERT_GUARD
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(90), nthreads=8)
+    assert_bits_equal(img, want, f"scheduled path, {mode}")
+    assert st.segments == segs
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
