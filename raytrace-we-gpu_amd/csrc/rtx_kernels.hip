@@ -89,7 +89,7 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
 #define RTX_DIAG_PIXEL 0
 #endif
-#ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-1 coop segments into wave_times[0..7]
+#ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
 #define RTX_DIAG_COOP 0
 #endif
 #ifndef RTX_SHADE_MERGE  // 1: Lambert and metal lanes share one scatter path
@@ -1193,9 +1193,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             else
                 __builtin_amdgcn_s_setprio(RTX_TAIL_PRIO);
 #if RTX_DIAG_COOP
-            unsigned long long *cp = H.tier == 1u ? cpa : nullptr;
+            unsigned long long *cp = H.tier == (uint32_t)RTX_DIAG_COOP ? cpa : nullptr;
             unsigned long long *ctqp = &ctq;
-            if (H.tier == 1u) {
+            if (H.tier == (uint32_t)RTX_DIAG_COOP) {
                 const unsigned long long tn = __builtin_readcyclecounter();
                 if (was_t1) cpa[4] += tn - ctq;
                 ctq = tn;
@@ -1223,7 +1223,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 cpa[3] += tn - ctq;
                 ctq = tn;
             }
-            was_t1 = H.tier == 1u;
+            was_t1 = H.tier == (uint32_t)RTX_DIAG_COOP;
 #endif
             if (H.tier == 0u) __builtin_amdgcn_s_setprio(0);  // a heavy wave keeps its priority
             RTX_PROF(3)

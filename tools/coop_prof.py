@@ -42,8 +42,8 @@ for R in a.parts:
     st = ctx.stats()
     v = ctx.wave_times(8).reshape(-1).astype(np.float64)
     segs = max(v[5], 1.0)
-    rep = {"parts": R, "part": p, "kernel_ms": round(st.kernel_ms / max(1, st.launches), 3),
-           "tier1_segments": int(v[5])}
+    rep = {"lib": os.path.basename(a.lib), "parts": R, "part": p,
+           "kernel_ms": round(st.kernel_ms / max(1, st.launches), 3), "segments": int(v[5])}
     for k, n in enumerate(names):
         rep[n + "_clk"] = round(v[k] / segs, 1)
     rep["total_clk"] = round(v[:5].sum() / segs, 1)
