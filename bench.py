@@ -136,11 +136,32 @@ def cpu_baseline(args, world, frame, gpu_image, budget_s):
         done += batch
     dt = time.perf_counter() - t0
     samples = len(done) * args.width * args.spp
+    # single-thread rate on a few of the same rows (report 1 thread too)
+    few = [H // 8, 3 * H // 8, 5 * H // 8, 7 * H // 8]
+    t1 = time.perf_counter()
+    oracle.render_rows(world, frame, np.array(few, np.uint32), nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{len(done)} full rows (x{args.width} px, spp {args.spp}) of the same frame, "
                       f"spread over the image, fp32 oracle (oracle/rtx_oracle.c), {threads} threads, "
-                      f"{dt:.1f} s"}, {"rows_checked": len(done), "values_differing": mism,
-                                       "bit_exact": mism == 0}
+                      f"{dt:.1f} s",
+            "single_thread": {"value": len(few) * args.width * args.spp / dt1 / 1e6, "unit": "Msamples/s",
+                              "sample": f"{len(few)} rows, 1 thread, {dt1:.1f} s"},
+            "host": host_cpu()}, {"rows_checked": len(done), "values_differing": mism, "bit_exact": mism == 0}
+
+
+def host_cpu():
+    """The box's CPU: logical CPUs visible and the model name."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
 
 
 def main():
