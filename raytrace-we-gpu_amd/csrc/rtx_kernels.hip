@@ -83,9 +83,6 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
 #define RTX_DIAG_PROF 0
 #endif
-#ifndef RTX_LPT_DEAL  // 1: deal the initial fill of the normal queue round-robin over the waves
-#define RTX_LPT_DEAL 0
-#endif
 #ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
 #define RTX_DIAG_PIXEL 0
 #endif
@@ -1037,11 +1034,6 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // segment); tier 2 = slots [k1, kh), up to kHeavy2 per wave. An idle wave
 // tries tier 1 first; a tier-2 wave tops itself up from tier 2. Returns the
 // wave's tier (0: not heavy any more).
-// Cost rank of normal-queue slot `slot` (inverse of deal_slot).
-__device__ __forceinline__ uint32_t slot_rank(uint32_t slot, uint32_t kh, uint32_t w) {
-    const uint32_t q = slot - kh;  // slot >= kh for normal-queue pixels
-    return q < w * 64u ? (q & 63u) * w + (q >> 6) : q;
-}
 constexpr uint32_t kHeavy1 = RTX_HEAVY1_WAVE;
 constexpr uint32_t kHeavy2 = RTX_HEAVY_WAVE;
 struct HeavyState {
@@ -1139,8 +1131,6 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
-    // waves the initial fill was dealt over (k_cost_scatter), for slot_rank
-    const uint32_t deal_w = RTX_LPT_DEAL && kPersist && P.perm ? min(gridDim.x * kRB, npix - kh) / 64u : 0u;
 #if RTX_DIAG_PROF
     // [0] refill clocks [1] hit_world [2] shade [3] tail mode [4] iterations [5] tail iterations
     // [6] active lanes summed over iterations
@@ -1234,7 +1224,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
-        if (__ballot(L.active && slot_rank(L.slot, kh, deal_w) < P.prio_slots) != 0ull)
+        if (__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull)
             __builtin_amdgcn_s_setprio(3);
         else
             __builtin_amdgcn_s_setprio(0);
@@ -1357,21 +1347,9 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // Positions: bucket start (prefix of the global counts) + a range the
 // block reserves in the bucket + the element's rank inside the block. The
 // order within a bucket is arbitrary; per-pixel results do not depend on it.
-// The first `fill` slots of the normal queue (after the kh heavy slots,
-// heavy[1]) are dealt round-robin over the waves of the initial fill: wave
-// w's 64 slots get ranks w, w + W, w + 2W, ... (W = fill / 64), so the
-// costliest lane-mode pixels are spread one per wave instead of packed into
-// the first waves (which share CUs and would fight over the same SIMDs).
-__device__ __forceinline__ uint32_t deal_slot(uint32_t pos, uint32_t kh, uint32_t nn) {
-    if (pos < kh) return pos;
-    const uint32_t q = pos - kh;
-    const uint32_t w = nn / 64u;  // waves dealt (whole ones)
-    if (q >= w * 64u) return pos;
-    return kh + (q % w) * 64u + q / w;
-}
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          const uint32_t *counts, uint32_t *cursors,
-                                                         uint32_t *perm, const uint32_t *heavy, uint32_t fill) {
+                                                         uint32_t *perm) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -1395,11 +1373,9 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
-    const uint32_t kh = heavy ? min(heavy[1], n) : 0u;
-    const uint32_t nn = min(fill, n - kh);
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) perm[deal_slot(start[key[k]] + rank[k], kh, RTX_LPT_DEAL ? nn : 0u)] = i;
+        if (i < n) perm[start[key[k]] + rank[k]] = i;
     }
 }
 
@@ -1611,14 +1587,11 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
         hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
         hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
-                           (const uint32_t *)(RTX_HEAVY_WAVE ? heavy : nullptr), blocks * kRB);
+                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
         KParams q = p;
         q.perm = sched.perm;
         q.state = RTX_LPT_RESUME ? sched.state : nullptr;
-        // the top ranks of the normal queue run at top priority: with the
-        // deal, ranks < W are lane 0 of every wave, so a fraction of W
-        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u / (RTX_LPT_DEAL ? 64u : 1u));
+        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u);
         q.heavy = RTX_HEAVY_WAVE ? heavy : nullptr;
         e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
