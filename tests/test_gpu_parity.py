@@ -404,6 +404,33 @@ def test_scheduled_path_with_frame_options(gpu_ctx, oracle, rtx, mode):
     assert st.segments == segs
 
 
+def test_scheduled_path_edge_cases(gpu_ctx, oracle, rtx):
+    """The scheduled path (spp >= 8) on tiny frames, an all-sky scene, depth
+    1 and a ragged final tile of a split: pre-pass, heavy split, resume."""
+    base = rtx.random_world(4, depth=6, spp=9)
+    empty = rtx.World(np.zeros((0, 4), np.float32), np.zeros(0, np.float32), np.zeros((0, 4), np.float32), 5, 12)
+    shallow = rtx.World(base.spheres, base.mat_types, base.mat_values, 1, 8)
+    for world, w, h in [(base, 1, 1), (base, 3, 2), (empty, 17, 9), (shallow, 40, 23), (base, 65, 3)]:
+        frame = rtx.camera_look_at(w, h, aspect=max(w / h, 0.1))
+        img, st = render_gpu(gpu_ctx, world, frame)
+        want, segs = oracle.render_rows(world, frame, np.arange(h))
+        assert_bits_equal(img, want, f"scheduled edge n={world.count} {w}x{h} spp={world.spp}")
+        assert st.segments == segs
+    # a split whose last tile is ragged: 23 rows in 4-row tiles over 3 parts
+    world, W, H, T, R = base, 40, 23, 4, 3
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(rtx.camera_look_at(W, H, aspect=W / H))
+    buf = gpu_ctx.alloc((H, W, 4))
+    for part in range(R):
+        rows = rtx.part_row_ids(H, T, part, R)
+        gpu_ctx.render_rows(T, part, R, buf.ptr)
+        gpu_ctx.sync()
+        got = buf.numpy().reshape(-1)[: len(rows) * W * 4].reshape(len(rows), W, 4)
+        want, _ = oracle.render_rows(world, rtx.camera_look_at(W, H, aspect=W / H), rows)
+        assert_bits_equal(got, want, f"ragged split part {part}")
+    buf.free()
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
