@@ -45,12 +45,13 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2
+VARIANTS := best prof ptime cprof cprof2 nosm
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
 VFLAGS_cprof2        := -DRTX_DIAG_COOP=2
+VFLAGS_nosm          := -DRTX_COOP_SM=0
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

@@ -143,7 +143,7 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 constexpr uint32_t kRB = RTX_BLOCK;
 static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64");
 #ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
-#define RTX_WAVES_PER_SIMD 0
+#define RTX_WAVES_PER_SIMD 5  // 96 VGPRs, no spills (the compiler's own choice is 100: 4 waves)
 #endif
 #if RTX_WAVES_PER_SIMD
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
@@ -776,6 +776,135 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
         return (int)(0xffffffffu - (uint32_t)kk);
     }
 }
+
+
+// Sphere-major group coop for 2..kSmRays rays (tier 2 and the frame tail).
+// The per-ray groups above give each lane one ray and a long run of spheres
+// (61 for 8 rays at C2), tested two at a time: latency-bound. Here lane l
+// tests spheres l, l+64, ... against every ray in turn (the rays' lines
+// are read from LDS once per ray), appends each flagged (sphere, ray) pair
+// to a wave list, and the wave then resolves the list, pairs spread over
+// all lanes, with the reference's ops (the body of resolve_one); every
+// accepted root is folded into its ray's key with an LDS atomic min on
+// (c bits << 32 | ~index), the (min c, largest index) rule of the in-order
+// scan. A non-finite root, or a list overflow (more than kSmCand pairs: an
+// unsafe line flags every sphere), sends the ray (the wave's rays) to the
+// exact sequential path. LDS per wave (coop_ws, 1280 B): rays [8][8] floats,
+// lines [8][8], keys [8] u64, bad [8], count, pairs [kSmCand].
+#ifndef RTX_COOP_SM  // multi-ray coop waves with at least this many rays use groups_sm (0 = never)
+#define RTX_COOP_SM 4
+#endif
+[[maybe_unused]] constexpr uint32_t kSmRays = 8, kSmCand = 160;
+static_assert((160 + kSmCand) * sizeof(float) <= kCoopWaveBytes, "sphere-major coop LDS");
+template <typename Q4>
+__device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,
+                                         f3 o, f3 d, float a, float inv_a, float t_min, float *ws, float &best,
+                                         bool &seq, unsigned long long *cp, unsigned long long *tq) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m = (uint32_t)__popcll(act);
+    const uint32_t rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    float *rays = ws;        // [kSmRays][8]: o, d, a, inv_a
+    float *lines = ws + 64;  // [kSmRays][8]: LineTest
+    unsigned long long *keys = reinterpret_cast<unsigned long long *>(ws + 128);
+    uint32_t *bad = reinterpret_cast<uint32_t *>(ws + 144);
+    uint32_t *count = reinterpret_cast<uint32_t *>(ws + 152);
+    uint32_t *pairs = reinterpret_cast<uint32_t *>(ws + 160);
+    if (active) {
+        float *w = rays + 8 * rank;
+        w[0] = o.x;
+        w[1] = o.y;
+        w[2] = o.z;
+        w[3] = d.x;
+        w[4] = d.y;
+        w[5] = d.z;
+        w[6] = a;
+        w[7] = inv_a;
+        const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+        float *t = lines + 8 * rank;
+        t[0] = T.ux;
+        t[1] = T.uz;
+        t[2] = T.vx;
+        t[3] = T.vy;
+        t[4] = T.vz;
+        t[5] = T.nou;
+        t[6] = T.nov;
+        t[7] = T.thr;
+        keys[rank] = ~0ull;
+        bad[rank] = 0u;
+    }
+    if (lane == 0u) *count = 0u;
+    __builtin_amdgcn_wave_barrier();
+    RTX_CP(0)
+    const uint32_t n = S.n;
+#pragma unroll 1
+    for (uint32_t r = 0; r < m; ++r) {
+        const float *t = lines + 8 * r;  // wave-uniform: kept in scalars
+        LineTest T;
+        T.ux = read_lane(t[0], 0);
+        T.uz = read_lane(t[1], 0);
+        T.vx = read_lane(t[2], 0);
+        T.vy = read_lane(t[3], 0);
+        T.vz = read_lane(t[4], 0);
+        T.nou = read_lane(t[5], 0);
+        T.nov = read_lane(t[6], 0);
+        T.thr = read_lane(t[7], 0);
+#pragma unroll 2
+        for (uint32_t j = lane; j < n; j += 64u) {
+            const float4 pq = sph4[j];
+            if (!(line_test_q(T, pq.x, pq.y, pq.z, pq.w) < T.thr)) {
+                const uint32_t k = atomicAdd(count, 1u);
+                if (k < kSmCand) pairs[k] = (j << 3) | r;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    RTX_CP(1)
+    const uint32_t K = *count;
+    const float inf = __uint_as_float(0x7f800000u);
+#pragma unroll 1
+    for (uint32_t k = lane; k < min(K, kSmCand); k += 64u) {
+        const uint32_t e = pairs[k];
+        const uint32_t j = e >> 3, r = e & 7u;
+        const float *w = rays + 8 * r;
+        const float4 pq = sph4[j];
+        const float rr = rad ? rad[j] : S.cen[j].w;
+        // resolve_one's ops for one candidate
+        const float ocx = w[0] - pq.x;
+        const float ocy = w[1] - pq.y;
+        const float ocz = w[2] - pq.z;
+        const float hb = fmaf(ocz, w[5], fmaf(ocy, w[4], ocx * w[3]));
+        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(rr * rr))));
+        const float disc = fmaf(hb, hb, -(w[6] * cc));
+        if (disc < 0.0f) continue;
+        const float sq = sqrtf(disc);
+        const float rn = (-hb - sq) * w[7];
+        const float rf = (-hb + sq) * w[7];
+        if (!(fabsf(rn) < inf && fabsf(rf) < inf)) {
+            atomicOr(&bad[r], 1u);
+            continue;
+        }
+        const bool use_n = !(rn < t_min);
+        const float c = use_n ? rn : rf;
+        if (use_n || !(rf < t_min))  // c >= t_min > 0: its bits order like its value
+            atomicMin(&keys[r], ((unsigned long long)__float_as_uint(c) << 32) | (unsigned long long)(0xffffffffu - j));
+    }
+    __builtin_amdgcn_wave_barrier();
+    RTX_CP(2)
+    seq = false;
+    if (!active) return -1;
+    if (K > kSmCand || bad[rank] != 0u) {
+        seq = true;
+        return -1;
+    }
+    const unsigned long long kk = keys[rank];
+    if (kk == ~0ull) return -1;
+    const float c = __uint_as_float((uint32_t)(kk >> 32));
+    if (!(c <= best)) return -1;  // accepted iff c <= t_max
+    best = c;
+    return (int)(0xffffffffu - (uint32_t)kk);
+}
+
 #undef RTX_CP
 
 template <typename Q4>
@@ -785,6 +914,13 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, const 
                                                 unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
     if (__popcll(act) == 1)
         return groups_impl<true>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
+#if RTX_COOP_SM
+    static_assert(RTX_COOP_MAX <= (int)kSmRays && RTX_HEAVY_WAVE <= (int)kSmRays, "coop waves hold <= 8 rays");
+    // 2-3 rays: groups of 32 or 16 lanes scan short chunks; from 4 rays on
+    // (chunks of 31+ spheres per lane) the sphere-major pass is faster
+    if (__popcll(act) >= RTX_COOP_SM)
+        return groups_sm(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, best, seq, cp, tq);
+#endif
     return groups_impl<false>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
 }
 
