@@ -267,7 +267,7 @@ def main():
                          "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                          "traffic": None if traffic is None else round(traffic),
-                         "kernel": ("rtx_render_rows launch = k_render<false,true> 1-spp cost pre-pass (sample 0, "
+                         "kernel": ("rtx_render_rows launch = k_render<false,true> 2-spp cost pre-pass (samples 0-1, "
                                     "resumed from) + k_cost_hist + k_heavy_split + k_cost_scatter + k_render<true> "
                                     "(cost-ordered persistent lanes, heavy-pixel coop tiers)")
                                    if args.spp >= 8 else "rtx_render_rows launch = k_render<false> (exact grid)",

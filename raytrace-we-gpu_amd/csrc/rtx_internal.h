@@ -80,8 +80,8 @@ struct KSchedule {
 #define RTX_LPT_BUCKETS 256
 #endif
 constexpr uint32_t kCostBuckets = RTX_LPT_BUCKETS;
-#ifndef RTX_LPT_SPP
-#define RTX_LPT_SPP 1
+#ifndef RTX_LPT_SPP  // pre-pass samples per pixel (kept: the render resumes after them)
+#define RTX_LPT_SPP 2
 #endif
 constexpr uint32_t kCostSpp = RTX_LPT_SPP;
 constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
