@@ -128,6 +128,12 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_HEAVY_RHO  // "small" frame share: fewer pixels than rho * resident lanes
 #define RTX_HEAVY_RHO 1.2
 #endif
+#ifndef RTX_HEAVY_RHO2  // "medium" frame share: fewer pixels than rho2 * resident lanes (0 = off)
+#define RTX_HEAVY_RHO2 2.0
+#endif
+#ifndef RTX_HEAVY2_ALPHA_MEDIUM  // tier 2 for a medium share: key > this * share
+#define RTX_HEAVY2_ALPHA_MEDIUM 1.5
+#endif
 #ifndef RTX_HEAVY1_ALPHA  // tier 1 iff key > alpha1 * a lane's share of the summed keys
 #define RTX_HEAVY1_ALPHA 1.7
 #endif
@@ -1532,7 +1538,10 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     const double share = w / (double)(lanes ? lanes : 1u);
     const bool small = (double)npix < RTX_HEAVY_RHO * (double)lanes;
     const double a1 = small ? RTX_HEAVY1_ALPHA_SMALL : RTX_HEAVY1_ALPHA;
-    const double a2 = small ? RTX_HEAVY_ALPHA : a1;
+    // a medium share (fewer than RTX_HEAVY_RHO2 pixels per lane, e.g. a
+    // 4-way split) also gets tier 2 above RTX_HEAVY2_ALPHA_MEDIUM x share
+    const bool medium = !small && (double)npix < RTX_HEAVY_RHO2 * (double)lanes;
+    const double a2 = small ? RTX_HEAVY_ALPHA : medium ? min(RTX_HEAVY2_ALPHA_MEDIUM, a1) : a1;
     uint32_t kh = 0, k1 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
