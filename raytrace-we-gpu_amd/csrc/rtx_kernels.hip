@@ -129,7 +129,7 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #define RTX_HEAVY_RHO 1.2
 #endif
 #ifndef RTX_HEAVY_RHO2  // "medium" frame share: fewer pixels than rho2 * resident lanes (0 = off)
-#define RTX_HEAVY_RHO2 2.0
+#define RTX_HEAVY_RHO2 3.5
 #endif
 #ifndef RTX_HEAVY2_ALPHA_MEDIUM  // tier 2 for a medium share: key > this * share
 #define RTX_HEAVY2_ALPHA_MEDIUM 1.5
@@ -1539,7 +1539,7 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     const bool small = (double)npix < RTX_HEAVY_RHO * (double)lanes;
     const double a1 = small ? RTX_HEAVY1_ALPHA_SMALL : RTX_HEAVY1_ALPHA;
     // a medium share (fewer than RTX_HEAVY_RHO2 pixels per lane, e.g. a
-    // 4-way split) also gets tier 2 above RTX_HEAVY2_ALPHA_MEDIUM x share
+    // 2- or 4-way split) also gets tier 2 above RTX_HEAVY2_ALPHA_MEDIUM x share
     const bool medium = !small && (double)npix < RTX_HEAVY_RHO2 * (double)lanes;
     const double a2 = small ? RTX_HEAVY_ALPHA : medium ? min(RTX_HEAVY2_ALPHA_MEDIUM, a1) : a1;
     uint32_t kh = 0, k1 = 0;
