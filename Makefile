@@ -13,7 +13,7 @@ LIB       := $(LIBDIR)/librtx.so
 CLI       := $(BINDIR)/rtx_cli
 HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)/rtx_prefilter.h
 
-all: $(LIB) $(CLI) oracle
+all: $(LIB) $(CLI) oracle $(LIBDIR)/variants/librtx_stress.so
 
 $(LIBDIR)/%.o: $(SRC)/%.hip $(HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -45,13 +45,16 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2 nosm
+VARIANTS := best prof ptime cprof cprof2 nosm stress
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
 VFLAGS_cprof2        := -DRTX_DIAG_COOP=2
 VFLAGS_nosm          := -DRTX_COOP_SM=0
+# test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and
+# fallback path runs all the time (tests/test_gpu_parity.py, stress tests)
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_SM_CAND=2
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

@@ -160,7 +160,10 @@ static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64"
 // Candidate list (RTX_DEFER): per lane kCand slots in LDS, slot-major
 // (slot j of lane t at [j * kRB + t]: conflict-free), plus one dump slot
 // that absorbs writes past the end (the lane then falls back, see below).
-constexpr int kCand = 12;
+#ifndef RTX_CAND  // candidate-list capacity per lane (entries; a full list is resolved in rounds)
+#define RTX_CAND 12
+#endif
+constexpr int kCand = RTX_CAND;
 constexpr uint32_t kListBytes = (kCand + 1) * kRB * sizeof(uint32_t);  // 13,312 B at 256
 static_assert(kListBytes % 16 == 0, "LDS carve must stay 16-byte aligned");
 
@@ -800,7 +803,10 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
 #ifndef RTX_COOP_SM  // multi-ray coop waves with at least this many rays use groups_sm (0 = never)
 #define RTX_COOP_SM 4
 #endif
-[[maybe_unused]] constexpr uint32_t kSmRays = 8, kSmCand = 160;
+#ifndef RTX_SM_CAND  // sphere-major coop: (sphere, ray) pairs per wave before the exact fallback
+#define RTX_SM_CAND 160
+#endif
+[[maybe_unused]] constexpr uint32_t kSmRays = 8, kSmCand = RTX_SM_CAND;
 static_assert((160 + kSmCand) * sizeof(float) <= kCoopWaveBytes, "sphere-major coop LDS");
 template <typename Q4>
 __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,

@@ -11,6 +11,7 @@ import os
 import numpy as np
 import pytest
 
+from cases import lambert_cases
 from conftest import GOLDEN
 from tolerance import check_hits_against_fp64
 
@@ -200,7 +201,6 @@ def test_random_world_frames_bit_exact(gpu_ctx, oracle, rtx, ext, w, h, spp, dep
 def test_lambert_guard_device(gpu_ctx, oracle):
     """RTX_FN_LAMBERT_DIR[_GUARD]: the kernel's diffuse direction equals the
     oracle's bit for bit; zero directions give NaN unguarded, the normal guarded."""
-    from test_oracle_golden import lambert_cases
     p, nrm, rius, nz = lambert_cases()
     for guard in (False, True):
         got = gpu_ctx.debug_lambert_dir(p, nrm, rius, guard)
@@ -429,6 +429,41 @@ def test_scheduled_path_edge_cases(gpu_ctx, oracle, rtx):
         want, _ = oracle.render_rows(world, rtx.camera_look_at(W, H, aspect=W / H), rows)
         assert_bits_equal(got, want, f"ragged split part {part}")
     buf.free()
+
+
+STRESS_LIB = os.path.join(os.path.dirname(GOLDEN), "..", "raytrace-we-gpu_amd", "lib", "variants",
+                          "librtx_stress.so")
+
+
+@pytest.fixture(scope="module")
+def stress_ctx(rtx):
+    """The stress build (make all): candidate lists of 1 entry and 2
+    sphere-major pairs, so resolve rounds, list overflows and the exact
+    sequential fallbacks run all the time."""
+    if not os.path.exists(STRESS_LIB):
+        pytest.skip("stress build missing: make all")
+    ctx = rtx.Context(0, lib=rtx.load_library(STRESS_LIB))
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("nparts,part", [(1, 0), (2, 1), (4, 2), (8, 5)])
+def test_overflow_and_fallback_paths_bit_exact(stress_ctx, oracle, rtx, nparts, part):
+    """Every share size (lane mode, tiers 1 and 2, tail coop) with every
+    overflow forced: the rows equal the oracle's bit for bit."""
+    world = rtx.random_world(11, depth=50, spp=12)
+    W, H, T = 320, 180, 5
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    stress_ctx.upload_world(world)
+    stress_ctx.set_frame(frame)
+    rows = rtx.part_row_ids(H, T, part, nparts)
+    buf = stress_ctx.alloc((H, W, 4))
+    stress_ctx.render_rows(T, part, nparts, buf.ptr)
+    stress_ctx.sync()
+    got = buf.numpy().reshape(-1)[: len(rows) * W * 4].reshape(len(rows), W, 4)
+    buf.free()
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
+    assert_bits_equal(got, want, f"stress build, part {part} of {nparts}")
 
 
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
