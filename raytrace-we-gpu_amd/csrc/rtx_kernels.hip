@@ -441,21 +441,50 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // first sphere | 8-bit mask << 24 (so n_pad <= 2^24, checked at upload).
 // Returns the block to resume at: nblk, or earlier once some lane's list is
 // full (kCand entries) and must be resolved first (wave-uniform).
+//
+// RTX_SCAN_PF 1: the block's 32 floats are double-buffered in SGPRs. The
+// next block's two s_load_dwordx16 are issued (inline asm: the compiler
+// otherwise sinks them to the end of the iteration and waits at once) before
+// this block's 33 VALU instructions and waited for after them, so a scalar
+// cache miss (every block of a large scene) runs under the block's compute.
+// Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
+// loaded registers ("+s") so that nothing reads them before it. Every path
+// out of the loop body passes a wait, so no load is in flight at exit.
+#ifndef RTX_SCAN_PF  // 0: no kPF kernels (every scene takes the plain scan)
+#define RTX_SCAN_PF 1
+#endif
+constexpr uint32_t kScanPfMin = 1024;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
+typedef float f16v __attribute__((ext_vector_type(16)));
+// Issue block p's loads; the "+v" operands (the line's basis, which every
+// VALU instruction of the scan reads) keep the compiler from scheduling the
+// previous block's compute above the issue.
+__device__ __forceinline__ void sload_blk(cfloat_p p, f16v &lo, f16v &hi, f2v &d0, f2v &d1, f2v &d2, f2v &d3,
+                                          f2v &d4, f2v &d5, f2v &d6) {
+    asm volatile("s_load_dwordx16 %0, %9, 0x0\n\ts_load_dwordx16 %1, %9, 0x40"
+                 : "=&s"(lo), "=&s"(hi), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6)
+                 : "s"(p));
+}
+__device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(lo), "+s"(hi));
+}
+template <bool kPF>
 __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk,
                                                    const LineTest &T, uint32_t *list, uint32_t &cnt) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
-    const f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
-    const f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
-    for (; b < nblk; ++b) {
-        const cfloat_p blk = pre + 32 * b;
+    f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
+    f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
+    const f2v th = {T.thr, T.thr};
+    // One 8-sphere block (blk(i) = its i-th float); true when some lane's
+    // list is full and the scan must stop after this block.
+    auto step = [&](auto blk, uint32_t bb) -> bool {
         f2v q[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const f2v cx = {blk[2 * p], blk[2 * p + 1]};
-            const f2v cy = {blk[8 + 2 * p], blk[9 + 2 * p]};
-            const f2v cz = {blk[16 + 2 * p], blk[17 + 2 * p]};
-            const f2v R = {blk[24 + 2 * p], blk[25 + 2 * p]};
+            const f2v cx = {blk(2 * p), blk(2 * p + 1)};
+            const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
+            const f2v cz = {blk(16 + 2 * p), blk(17 + 2 * p)};
+            const f2v R = {blk(24 + 2 * p), blk(25 + 2 * p)};
             const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
             const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
             q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
@@ -477,12 +506,37 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
                 inv = (inv << 1) | (__float_as_uint(s.x) >> 31);
             }
             const uint32_t mask = ~inv & 0xffu;
-            my[cnt * kRB] = (8u * b) | (mask << 24);  // cnt < kCand here
+            my[cnt * kRB] = (8u * bb) | (mask << 24);  // cnt < kCand here
             cnt += mask != 0u ? 1u : 0u;
-            if (__ballot(cnt == (uint32_t)kCand) != 0ull) return b + 1;
+            return __ballot(cnt == (uint32_t)kCand) != 0ull;
         }
+        return false;
+    };
+    if constexpr (kPF) {
+    // ping-pong between two SGPR buffers (no copies): A holds block b
+    if (b >= nblk) return nblk;
+    f16v a_lo, a_hi, b_lo, b_hi;
+    sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
+    sload_wait(a_lo, a_hi);
+    for (;;) {
+        sload_blk(pre + 32 * min(b + 1, nblk - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, nov);
+        bool full = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
+        sload_wait(b_lo, b_hi);
+        if (full) return b + 1;
+        if (++b >= nblk) return nblk;
+        sload_blk(pre + 32 * min(b + 1, nblk - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
+        full = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
+        sload_wait(a_lo, a_hi);
+        if (full) return b + 1;
+        if (++b >= nblk) return nblk;
+    }
+    } else {
+    for (; b < nblk; ++b) {
+        const cfloat_p blk = pre + 32 * b;
+        if (step([&](int i) { return blk[i]; }, b)) return b + 1;
     }
     return nblk;
+    }
 }
 
 // Resolve the lane's list (m entries: first sphere index | mask << 24)
@@ -548,6 +602,7 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // lane's list is full); the (min c, largest index) rule is
 // order-independent, so rounds compose. A non-finite root takes
 // hit_blocks_seq.
+template <bool kPF>
 __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
                                              float t_min, float &best, uint32_t *list) {
     const cfloat_p pre = (cfloat_p)S.pre;
@@ -559,7 +614,7 @@ __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float 
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = scan_prefilter(pre, b, nblk, T, list, cnt);
+        b = scan_prefilter<kPF>(pre, b, nblk, T, list, cnt);
         ok = resolve_pre(S.cen, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx) && ok;
     } while (b < nblk);
     if (!ok) {
@@ -572,10 +627,11 @@ __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float 
 
 // One ray segment against the whole scene with sphere data read through
 // scalar loads (RTX_SRC 1 and the debug kernel).
+template <bool kPF = false>
 __device__ __forceinline__ int trace_scalar(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
                                             float &best, uint32_t *list) {
 #if RTX_PREFILTER
-    return hit_world_pre(S, o, d, a, inv_a, t_min, best, list);
+    return hit_world_pre<kPF>(S, o, d, a, inv_a, t_min, best, list);
 #else
     return hit_world((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1, list);
 #endif
@@ -1230,7 +1286,7 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
-template <bool kPersist, bool kCost = false>
+template <bool kPersist, bool kCost = false, bool kPF = false>
 __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     // dynamic LDS: [candidate list, kListBytes][coop rays, kCoopBytes][sphere blocks (RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -1351,7 +1407,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
-                    my_hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
+                    my_hit = trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
                 shade<kCost>(P, F, L, min(my_hit, last), my_best);
             }
@@ -1382,7 +1438,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 #if RTX_SRC == 0
             const int hit = hit_world(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
 #else
-            const int hit = trace_scalar(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+            const int hit = trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
 #endif
             RTX_PROF(1)
             shade<kCost>(P, F, L, min(hit, last), best);
@@ -1595,7 +1651,9 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx = min(trace_scalar(S, o, d, a, inv_a, t_min, best, list), (int)S.n - 1);
+    const int idx = min((RTX_SCAN_PF && S.n_pad > kScanPfMin ? trace_scalar<true>(S, o, d, a, inv_a, t_min, best, list)
+                                                             : trace_scalar<false>(S, o, d, a, inv_a, t_min, best, list)),
+                        (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
         for (int k = 0; k < 10; ++k) r[k] = 0.0f;
@@ -1674,14 +1732,30 @@ static hipError_t allow_lds(const void *kern, size_t lds) {
     return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
+// k_render with the SGPR double-buffered scan for scenes whose `pre` array
+// does not stay in the scalar cache (RTX_SCAN_PF, kScanPfMin).
+static bool use_pf(const KScene &s) { return RTX_SCAN_PF && s.n_pad > kScanPfMin; }
+template <bool kPersist, bool kCost>
+static const void *render_fn(bool pf) {
+    return pf ? (const void *)k_render<kPersist, kCost, true> : (const void *)k_render<kPersist, kCost, false>;
+}
+template <bool kPersist, bool kCost>
+static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, const KParams &a) {
+    if (pf)
+        hipLaunchKernelGGL((k_render<kPersist, kCost, true>), dim3(blocks), dim3(kRB), lds, stream, a);
+    else
+        hipLaunchKernelGGL((k_render<kPersist, kCost, false>), dim3(blocks), dim3(kRB), lds, stream, a);
+}
+
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
     if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
     const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
-    hipError_t e = allow_lds((const void *)k_render<false, true>, lds);
+    const bool pf = use_pf(p.scene);
+    hipError_t e = allow_lds(render_fn<false, true>(pf), lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_render<false, true>), dim3(ceil_div(lanes, kRB)), dim3(kRB), lds, stream, p);
+    launch_k<false, true>(pf, ceil_div(lanes, kRB), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -1696,13 +1770,14 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     hipError_t e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
         const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
-        e = allow_lds((const void *)k_render<true>, lds);
-        if (e == hipSuccess) e = allow_lds((const void *)k_render<false>, lds);
-        if (e == hipSuccess) e = allow_lds((const void *)k_render<true, true>, lds);
-        if (e == hipSuccess) e = allow_lds((const void *)k_render<false, true>, lds);
+        const bool pf = use_pf(p.scene);
+        e = allow_lds(render_fn<true, false>(pf), lds);
+        if (e == hipSuccess) e = allow_lds(render_fn<false, false>(pf), lds);
+        if (e == hipSuccess) e = allow_lds(render_fn<true, true>(pf), lds);
+        if (e == hipSuccess) e = allow_lds(render_fn<false, true>(pf), lds);
         if (e != hipSuccess) return e;
         if (!RTX_PERSISTENT || !sched.cost || p.spp < kLptMinSpp) {
-            hipLaunchKernelGGL(k_render<false>, dim3(need), dim3(kRB), lds, stream, p);
+            launch_k<false, false>(pf, need, lds, stream, p);
             return hipGetLastError();
         }
         if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
@@ -1723,10 +1798,10 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
 #if RTX_LPT_PERSIST_PREPASS
         // persistent lanes: a lane whose pixel ends takes the next one, so the
         // pass does not wait on each wave's slowest pixel
-        const uint32_t cblocks = min(need, resident_blocks((const void *)k_render<true, true>, lds));
-        hipLaunchKernelGGL((k_render<true, true>), dim3(cblocks), dim3(kRB), lds, stream, c);
+        const uint32_t cblocks = min(need, resident_blocks(render_fn<true, true>(pf), lds));
+        launch_k<true, true>(pf, cblocks, lds, stream, c);
 #else
-        hipLaunchKernelGGL((k_render<false, true>), dim3(need), dim3(kRB), lds, stream, c);
+        launch_k<false, true>(pf, need, lds, stream, c);
 #endif
         // 2. counting sort by cost, descending
         const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
@@ -1734,7 +1809,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
                            p.rows_local, sched.buckets);
         // 3. heavy-pixel split (from the histogram), the ordered queue, then
         // the persistent render over it
-        const uint32_t blocks = min(need, resident_blocks((const void *)k_render<true>, lds));
+        const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
         uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
         hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
         hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
@@ -1746,7 +1821,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         q.heavy = RTX_HEAVY_WAVE ? heavy : nullptr;
         e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_render<true>, dim3(blocks), dim3(kRB), lds, stream, q);
+        launch_k<true, false>(pf, blocks, lds, stream, q);
     } else {
         const size_t lds = kListBytes + kChunk * sizeof(float4);
         e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);

@@ -466,6 +466,31 @@ def test_overflow_and_fallback_paths_bit_exact(stress_ctx, oracle, rtx, nparts, 
     assert_bits_equal(got, want, f"stress build, part {part} of {nparts}")
 
 
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+def test_double_buffered_scan_bit_exact(request, oracle, rtx, ctx_name):
+    """Scenes above kScanPfMin (1024 padded spheres) take the kernels whose
+    scan double-buffers each 8-sphere block in SGPRs (RTX_SCAN_PF): the
+    scheduled path (pre-pass + persistent render, spp >= 8) and hit_world
+    on random rays. With the stress build every candidate fills the list,
+    so the scan leaves early after nearly every flagged block."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(20, depth=50, spp=8)
+    assert world.count > 1024
+    frame = rtx.camera_look_at(96, 54, aspect=96 / 54)
+    img, st = render_gpu(ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(54), nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img, want, f"{ctx_name}: {world.count} spheres")
+    assert st.segments == segs
+    rng = np.random.default_rng(11)
+    o = np.concatenate([rng.uniform(-20, 20, (4000, 1)), rng.uniform(0.1, 6, (4000, 1)),
+                        rng.uniform(-20, 20, (4000, 1))], 1)
+    d = rng.normal(size=(4000, 3))
+    d[:, 1] = -np.abs(d[:, 1]) * 0.3
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    got = ctx.debug_hit_world(rays)
+    assert_bits_equal(got, oracle.hit_world_f32(world, rays), f"{ctx_name}: hit_world")
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
