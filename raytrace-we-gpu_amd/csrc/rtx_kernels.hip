@@ -149,7 +149,9 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 constexpr uint32_t kRB = RTX_BLOCK;
 static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64");
 #ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
-#define RTX_WAVES_PER_SIMD 5  // 96 VGPRs, no spills (the compiler's own choice is 100: 4 waves)
+#define RTX_WAVES_PER_SIMD 5  // 96 VGPRs (the compiler's own choice is 100: 4 waves); the
+                              // few spills (SGPRs to VGPR lanes, ~7 VGPR dwords to scratch) sit in
+                              // per-segment and coop code, none in the scan or resolve loops
 #endif
 #if RTX_WAVES_PER_SIMD
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
@@ -450,6 +452,9 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
 // loaded registers ("+s") so that nothing reads them before it. Every path
 // out of the loop body passes a wait, so no load is in flight at exit.
+#ifndef RTX_RESOLVE_LDS  // 1: lane-mode resolve reads sphere data from the block's LDS copy (small scenes)
+#define RTX_RESOLVE_LDS 1
+#endif
 #ifndef RTX_SCAN_PF  // 0: no kPF kernels (every scene takes the plain scan)
 #define RTX_SCAN_PF 1
 #endif
@@ -602,9 +607,11 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // lane's list is full); the (min c, largest index) rule is
 // order-independent, so rounds compose. A non-finite root takes
 // hit_blocks_seq.
-template <bool kPF>
-__device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
-                                             float t_min, float &best, uint32_t *list) {
+// `ld(i)` returns (center, radius) of sphere i for the resolve (cen in HBM,
+// or the block's LDS copy of the coop's sphere data, RTX_RESOLVE_LDS).
+template <bool kPF, typename Ld>
+__device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
+                                                float t_min, float &best, uint32_t *list) {
     const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
@@ -615,7 +622,7 @@ __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float 
     do {
         uint32_t cnt;
         b = scan_prefilter<kPF>(pre, b, nblk, T, list, cnt);
-        ok = resolve_pre(S.cen, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx) && ok;
+        ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx) && ok;
     } while (b < nblk);
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
@@ -623,6 +630,12 @@ __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float 
         idx = hit_blocks_seq((cfloat_p)S.soa, nblk, 0, o, d, a, inv_a, t_min, best, -1);
     }
     return idx;
+}
+template <bool kPF>
+__device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
+                                             float t_min, float &best, uint32_t *list) {
+    const float4 *__restrict__ cen = S.cen;
+    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list);
 }
 
 // One ray segment against the whole scene with sphere data read through
@@ -1437,6 +1450,17 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             float best = __uint_as_float(0x7f800000u);
 #if RTX_SRC == 0
             const int hit = hit_world(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
+#elif RTX_PREFILTER && RTX_RESOLVE_LDS
+            // scenes that fit the coop's LDS copy resolve their candidates
+            // from it (same centre floats, cen.w = s_rad) instead of HBM/L2
+            const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
+                                ? hit_world_pre_ld<kPF>(P.scene,
+                                                        [s_pre4, s_rad](uint32_t i) {
+                                                            const float4 c = s_pre4[i];
+                                                            return make_float4(c.x, c.y, c.z, s_rad[i]);
+                                                        },
+                                                        L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                                : trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
 #else
             const int hit = trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
 #endif
