@@ -151,7 +151,7 @@ static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64"
 #ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
 #define RTX_WAVES_PER_SIMD 5  // 96 VGPRs (the compiler's own choice is 100: 4 waves); the
                               // few spills (SGPRs to VGPR lanes, ~7 VGPR dwords to scratch) sit in
-                              // per-segment and coop code, none in the scan or resolve loops
+                              // per-segment and coop code, none in the lane-mode scan loop
 #endif
 #if RTX_WAVES_PER_SIMD
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
