@@ -45,7 +45,7 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl
+VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
@@ -56,6 +56,8 @@ VFLAGS_nosm          := -DRTX_COOP_SM=0
 VFLAGS_nopf          := -DRTX_SCAN_PF=0
 # lane-mode resolve from cen in HBM (rtx_kernels.hip RTX_RESOLVE_LDS)
 VFLAGS_noresl        := -DRTX_RESOLVE_LDS=0
+# one-ray coop: flag a window, then resolve (RTX_ONE_DEFER; measured no better)
+VFLAGS_defer         := -DRTX_ONE_DEFER=1
 # test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and
 # fallback path runs all the time (tests/test_gpu_parity.py, stress tests)
 VFLAGS_stress        := -DRTX_CAND=1 -DRTX_SM_CAND=2

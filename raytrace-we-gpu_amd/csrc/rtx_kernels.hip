@@ -667,7 +667,14 @@ constexpr uint32_t kCoopBytes = (kRB / 64) * kCoopWaveBytes;
 #ifndef RTX_COOP_STEP
 #define RTX_COOP_STEP 2
 #endif
-constexpr uint32_t kCoopStep = RTX_COOP_STEP;  // spheres per coop step (reads in flight)
+constexpr uint32_t kCoopStep = RTX_COOP_STEP;
+#ifndef RTX_ONE_DEFER  // one-ray coop: flag a window, then resolve (1) / resolve on the spot (0)
+#define RTX_ONE_DEFER 0  // 1 measured no better
+#endif
+#ifndef RTX_ONE_STEP  // one-ray coop, deferred: spheres per scan step (reads in flight)
+#define RTX_ONE_STEP 4
+#endif
+[[maybe_unused]] constexpr uint32_t kOneStep = RTX_ONE_STEP;  // spheres per coop step (reads in flight)
 constexpr uint32_t kCoopLds = 704;  // scenes up to this many spheres keep pre4 + radii in LDS for the coop (<= 13.75 KiB: 5 blocks/CU)
 static_assert(RTX_COOP_MAX <= (int)kCoopSlots, "RTX_COOP_MAX must be <= 32");
 
@@ -761,6 +768,38 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
         const f3 ro = mk3(read_lane(w[0], 0), read_lane(w[1], 0), read_lane(w[2], 0));
         const f3 rd = mk3(read_lane(w[3], 0), read_lane(w[4], 0), read_lane(w[5], 0));
         const float ra = read_lane(w[6], 0), ria = read_lane(w[7], 0);
+#if RTX_ONE_DEFER
+        // windows of up to 32 spheres per lane: scan the window (kOneStep
+        // reads in flight) into a flag mask, then resolve the flags, one per
+        // lane per pass, so the wave pays one resolve latency per pass
+        // rather than one per scan step in which any lane flagged
+        for (;;) {
+            if (__ballot(i < i1) == 0ull) break;
+            const uint32_t w0 = i, we = min(i1, w0 + 32u);
+            uint32_t fm = 0;
+            for (;;) {
+                const bool more = i < we;
+                if (__ballot(more) == 0ull) break;
+                float4 pq[kOneStep];
+#pragma unroll
+                for (uint32_t u = 0; u < kOneStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
+#pragma unroll
+                for (uint32_t u = 0; u < kOneStep; ++u)
+                    if (i + u < we && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr))
+                        fm |= 1u << (i + u - w0);
+                i = more ? i + kOneStep : i;
+            }
+            i = w0 < i1 ? we : w0;
+            while (__ballot(fm != 0u) != 0ull) {
+                const bool live = fm != 0u;
+                const uint32_t j = min(w0 + (uint32_t)__builtin_ctz(live ? fm : 1u), n - 1u);
+                fm &= fm - 1u;
+                const float4 pj = sph4[j];
+                const float rr = rad ? rad[j] : S.cen[j].w;
+                resolve_one(make_float4(pj.x, pj.y, pj.z, rr), (int)j, live, ro, rd, ra, ria, t_min, bc, bg, ok);
+            }
+        }
+#else
         for (;;) {
             const bool more = i < i1;
             if (__ballot(more) == 0ull) break;
@@ -778,6 +817,7 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
             }
             i = more ? i + kCoopStep : i;
         }
+#endif
     } else do {
         uint32_t cnt = 0;
         for (;;) {
