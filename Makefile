@@ -45,7 +45,7 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer
+VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer cand24 cand6
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
@@ -58,6 +58,9 @@ VFLAGS_nopf          := -DRTX_SCAN_PF=0
 VFLAGS_noresl        := -DRTX_RESOLVE_LDS=0
 # one-ray coop: flag a window, then resolve (RTX_ONE_DEFER; measured no better)
 VFLAGS_defer         := -DRTX_ONE_DEFER=1
+# candidate-list length (entries of 8 spheres per lane before a resolve round)
+VFLAGS_cand24        := -DRTX_CAND=24
+VFLAGS_cand6         := -DRTX_CAND=6
 # test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and
 # fallback path runs all the time (tests/test_gpu_parity.py, stress tests)
 VFLAGS_stress        := -DRTX_CAND=1 -DRTX_SM_CAND=2

@@ -19,7 +19,10 @@ sys.path.insert(0, os.path.join(ROOT, "raytrace-we-gpu_amd"))
 import rtx  # noqa: E402
 
 libs = sys.argv[1:] or [os.path.join(ROOT, "raytrace-we-gpu_amd/lib/variants/librtx_prof.so")]
-world = rtx.random_world(11, depth=50, spp=100)
+# C2 by default; RTX_SPROF_GRID / _CAP / _SPP select another scene (C5: 159, 100000, 16)
+world = rtx.random_world(int(os.environ.get("RTX_SPROF_GRID", "11")),
+                         capacity=int(os.environ.get("RTX_SPROF_CAP", "0")) or None, depth=50,
+                         spp=int(os.environ.get("RTX_SPROF_SPP", "100")))
 frame = rtx.camera_look_at(1920, 1080, aspect=1920 / 1080)
 for path in libs:
     c = rtx.Context(0, lib=rtx.load_library(path))
