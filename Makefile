@@ -45,7 +45,7 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer cand24 cand6
+VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer cand24 cand6 pfcand12
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
@@ -61,9 +61,10 @@ VFLAGS_defer         := -DRTX_ONE_DEFER=1
 # candidate-list length (entries of 8 spheres per lane before a resolve round)
 VFLAGS_cand24        := -DRTX_CAND=24
 VFLAGS_cand6         := -DRTX_CAND=6
+VFLAGS_pfcand12      := -DRTX_CAND_PF=12
 # test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and
 # fallback path runs all the time (tests/test_gpu_parity.py, stress tests)
-VFLAGS_stress        := -DRTX_CAND=1 -DRTX_SM_CAND=2
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_SM_CAND=2
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

@@ -168,6 +168,16 @@ static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64"
 constexpr int kCand = RTX_CAND;
 constexpr uint32_t kListBytes = (kCand + 1) * kRB * sizeof(uint32_t);  // 13,312 B at 256
 static_assert(kListBytes % 16 == 0, "LDS carve must stay 16-byte aligned");
+// The kPF kernels (scenes > kScanPfMin, no LDS sphere copy) have the LDS to
+// spare for longer lists: fewer scan pauses on large scenes (C5).
+#ifndef RTX_CAND_PF
+#define RTX_CAND_PF 24
+#endif
+template <bool kPF>
+constexpr uint32_t cand_of() { return kPF ? (uint32_t)RTX_CAND_PF : (uint32_t)kCand; }
+template <bool kPF>
+constexpr uint32_t list_bytes() { return (cand_of<kPF>() + 1) * kRB * sizeof(uint32_t); }
+static_assert(list_bytes<true>() % 16 == 0 && RTX_CAND_PF >= 1, "LDS carve must stay 16-byte aligned");
 
 #if RTX_DIAG_PROF
 // Diagnostic event counters, one set per wave in LDS: [0] batches scanned
@@ -513,7 +523,7 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
             const uint32_t mask = ~inv & 0xffu;
             my[cnt * kRB] = (8u * bb) | (mask << 24);  // cnt < kCand here
             cnt += mask != 0u ? 1u : 0u;
-            return __ballot(cnt == (uint32_t)kCand) != 0ull;
+            return __ballot(cnt == cand_of<kPF>()) != 0ull;
         }
         return false;
     };
@@ -578,7 +588,8 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
 // `ld(i)` returns (center, radius) of sphere i < n.
 template <typename Ld>
 __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t *list, uint32_t m, f3 o, f3 d,
-                                              float a, float inv_a, float t_min, float &best, int &idx) {
+                                              float a, float inv_a, float t_min, float &best, int &idx,
+                                              uint32_t cap = (uint32_t)kCand) {
     bool ok = true;
     uint32_t j = 0;
     uint32_t e = list[threadIdx.x];  // entry 0 (unused when m == 0)
@@ -590,7 +601,7 @@ __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t 
         e &= e - (1u << 24);  // drop that candidate from the mask
         const bool adv = live && (e >> 24) == 0u;
         j += adv ? 1u : 0u;
-        const uint32_t nx = list[min(j, (uint32_t)kCand) * kRB + threadIdx.x];
+        const uint32_t nx = list[min(j, cap) * kRB + threadIdx.x];
         e = adv ? nx : e;
         resolve_one(ld(min(i, n - 1u)), (int)i, live, o, d, a, inv_a, t_min, best, idx, ok);
     }
@@ -622,7 +633,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     do {
         uint32_t cnt;
         b = scan_prefilter<kPF>(pre, b, nblk, T, list, cnt);
-        ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx) && ok;
+        ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
     } while (b < nblk);
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
@@ -1341,14 +1352,15 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
 template <bool kPersist, bool kCost = false, bool kPF = false>
 __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
-    // dynamic LDS: [candidate list, kListBytes][coop rays, kCoopBytes][sphere blocks (RTX_SRC 0)]
+    // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][sphere data (coop LDS copy / RTX_SRC 0)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    float *coop_ws = reinterpret_cast<float *>(s_mem + kListBytes) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
+    constexpr uint32_t kLB = list_bytes<kPF>();
+    float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
     (void)coop_ws;
 #if RTX_SRC == 1
     // the coop's sphere data: a block-wide LDS copy of pre4 for small scenes
-    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kListBytes + kCoopBytes);
+    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
     float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
     const bool coop_lds = P.scene.n <= kCoopLds;
     if (coop_lds) {
@@ -1362,7 +1374,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const int last = (int)P.scene.n - 1;
 #if RTX_SRC == 0
     const uint32_t nblk = P.scene.n_pad / 8;
-    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes + kCoopBytes);
+    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
     const float *s_blk = reinterpret_cast<const float *>(s_blk4);
     const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
     for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kRB) s_blk4[i] = g4[i];
@@ -1707,7 +1719,8 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
 __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const float *rays,
                                                             uint32_t nrays, float t_min,
                                                             float t_max, float *out) {
-    __shared__ uint32_t list[kListBytes / sizeof(uint32_t)];
+    __shared__ uint32_t list[list_bytes<true>() > kListBytes ? list_bytes<true>() / sizeof(uint32_t)
+                                                             : kListBytes / sizeof(uint32_t)];
     const uint32_t i = blockIdx.x * kRB + threadIdx.x;
     if (i >= nrays) return;
     const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
@@ -1815,8 +1828,8 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
     if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
-    const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
     const bool pf = use_pf(p.scene);
+    const size_t lds = (pf ? list_bytes<true>() : kListBytes) + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
     hipError_t e = allow_lds(render_fn<false, true>(pf), lds);
     if (e != hipSuccess) return e;
     launch_k<false, true>(pf, ceil_div(lanes, kRB), lds, stream, p);
@@ -1833,8 +1846,8 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     }
     hipError_t e;
     if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
-        const size_t lds = kListBytes + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
         const bool pf = use_pf(p.scene);
+        const size_t lds = (pf ? list_bytes<true>() : kListBytes) + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
         e = allow_lds(render_fn<true, false>(pf), lds);
         if (e == hipSuccess) e = allow_lds(render_fn<false, false>(pf), lds);
         if (e == hipSuccess) e = allow_lds(render_fn<true, true>(pf), lds);
