@@ -491,6 +491,31 @@ def test_double_buffered_scan_bit_exact(request, oracle, rtx, ctx_name):
     assert_bits_equal(got, oracle.hit_world_f32(world, rays), f"{ctx_name}: hit_world")
 
 
+def test_scan_kernel_choice_boundary(gpu_ctx, oracle, rtx):
+    """n = 1024 (plain scan) and 1025 (n_pad 1032: kPF scan) on the same
+    rays, random spheres with duplicates (ties), small frames through the
+    scheduled path: bit-exact on both sides of kScanPfMin."""
+    rng = np.random.default_rng(5)
+    for n in (1024, 1025):
+        sph = np.concatenate([rng.uniform(-12, 12, (n, 1)), rng.uniform(-1, 3, (n, 1)),
+                              rng.uniform(-12, 12, (n, 1)), rng.uniform(0.1, 0.6, (n, 1))], 1).astype(np.float32)
+        sph[n - 1] = sph[3]
+        mt = rng.integers(0, 3, n).astype(np.float32)
+        mv = np.concatenate([rng.uniform(0.2, 1.0, (n, 3)), rng.uniform(1.2, 1.6, (n, 1))], 1).astype(np.float32)
+        world = rtx.World(sph, mt, mv, 20, 8)
+        gpu_ctx.upload_world(world)
+        o = np.concatenate([rng.uniform(-14, 14, (3000, 1)), rng.uniform(0, 5, (3000, 1)),
+                            rng.uniform(-14, 14, (3000, 1))], 1)
+        d = rng.normal(size=(3000, 3))
+        rays = np.concatenate([o, d], 1).astype(np.float32)
+        assert_bits_equal(gpu_ctx.debug_hit_world(rays), oracle.hit_world_f32(world, rays), f"n={n} hit_world")
+        frame = rtx.camera_look_at(64, 36, aspect=64 / 36)
+        img, st = render_gpu(gpu_ctx, world, frame)
+        want, segs = oracle.render_rows(world, frame, np.arange(36), nthreads=min(16, os.cpu_count() or 1))
+        assert_bits_equal(img, want, f"n={n} frame")
+        assert st.segments == segs
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
