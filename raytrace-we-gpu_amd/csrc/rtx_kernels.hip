@@ -528,29 +528,29 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
         return false;
     };
     if constexpr (kPF) {
-    // ping-pong between two SGPR buffers (no copies): A holds block b
-    if (b >= nblk) return nblk;
-    f16v a_lo, a_hi, b_lo, b_hi;
-    sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
-    sload_wait(a_lo, a_hi);
-    for (;;) {
-        sload_blk(pre + 32 * min(b + 1, nblk - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, nov);
-        bool full = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
-        sload_wait(b_lo, b_hi);
-        if (full) return b + 1;
-        if (++b >= nblk) return nblk;
-        sload_blk(pre + 32 * min(b + 1, nblk - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
-        full = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
+        // ping-pong between two SGPR buffers (no copies): A holds block b
+        if (b >= nblk) return nblk;
+        f16v a_lo, a_hi, b_lo, b_hi;
+        sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
         sload_wait(a_lo, a_hi);
-        if (full) return b + 1;
-        if (++b >= nblk) return nblk;
-    }
+        for (;;) {
+            sload_blk(pre + 32 * min(b + 1, nblk - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, nov);
+            bool full = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
+            sload_wait(b_lo, b_hi);
+            if (full) return b + 1;
+            if (++b >= nblk) return nblk;
+            sload_blk(pre + 32 * min(b + 1, nblk - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
+            full = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
+            sload_wait(a_lo, a_hi);
+            if (full) return b + 1;
+            if (++b >= nblk) return nblk;
+        }
     } else {
-    for (; b < nblk; ++b) {
-        const cfloat_p blk = pre + 32 * b;
-        if (step([&](int i) { return blk[i]; }, b)) return b + 1;
-    }
-    return nblk;
+        for (; b < nblk; ++b) {
+            const cfloat_p blk = pre + 32 * b;
+            if (step([&](int i) { return blk[i]; }, b)) return b + 1;
+        }
+        return nblk;
     }
 }
 
