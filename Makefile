@@ -45,19 +45,12 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best prof ptime cprof cprof2 nosm stress nopf noresl defer cand24 cand6 pfcand12
+VARIANTS := best prof ptime cprof cprof2 stress cand24 cand6 pfcand12
 VFLAGS_best          :=
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
 VFLAGS_cprof2        := -DRTX_DIAG_COOP=2
-VFLAGS_nosm          := -DRTX_COOP_SM=0
-# the scan without the SGPR double buffer (rtx_kernels.hip RTX_SCAN_PF)
-VFLAGS_nopf          := -DRTX_SCAN_PF=0
-# lane-mode resolve from cen in HBM (rtx_kernels.hip RTX_RESOLVE_LDS)
-VFLAGS_noresl        := -DRTX_RESOLVE_LDS=0
-# one-ray coop: flag a window, then resolve (RTX_ONE_DEFER; measured no better)
-VFLAGS_defer         := -DRTX_ONE_DEFER=1
 # candidate-list length (entries of 8 spheres per lane before a resolve round)
 VFLAGS_cand24        := -DRTX_CAND=24
 VFLAGS_cand6         := -DRTX_CAND=6

@@ -78,38 +78,72 @@ def probe(args):
         ctx.sync()
 
 
+def _pmc_pass(args, counters, tag):
+    """One rocprofv3 --pmc pass over the --probe child (one frame through
+    the C-ABI). Returns {counter: summed value over the k_render dispatches},
+    or raises RuntimeError."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        raise RuntimeError("rocprofv3 not found")
+    base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
+            "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
+            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", args.rng]
+    out = tempfile.mkdtemp(prefix=f"rtx_pmc_{tag}_")
+    cmd = [exe, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=240)
+        vals = {c: 0.0 for c in counters}
+        seen = set()
+        for path in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
+            for row in csv.DictReader(open(path)):
+                if "k_render" in row.get("Kernel_Name", "") and row.get("Counter_Name") in vals:
+                    vals[row["Counter_Name"]] += float(row["Counter_Value"])
+                    seen.add(row["Counter_Name"])
+        if seen != set(counters):
+            raise RuntimeError(f"no k_render rows for {sorted(set(counters) - seen)}")
+        return vals
+    except subprocess.SubprocessError as e:
+        raise RuntimeError(f"rocprofv3 {tag} failed: {type(e).__name__}") from e
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
 def pmc_traffic(args):
     """HBM bytes per render launch from rocprofv3 PMC counters, per
     MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes
     (TCC slots), KB units, FETCH_SIZE x2 on gfx950 for wide coalesced reads.
     Returns (bytes, details) or (None, reason)."""
-    exe = shutil.which("rocprofv3")
-    if not exe:
-        return None, "rocprofv3 not found"
-    vals = {}
-    base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
-            "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
-            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", args.rng]
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        out = tempfile.mkdtemp(prefix="rtx_pmc_")
-        cmd = [exe, "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
-        try:
-            subprocess.run(cmd, check=True, capture_output=True, timeout=240)
-        except Exception as e:  # noqa: BLE001
-            return None, f"rocprofv3 {ctr} failed: {type(e).__name__}"
-        total, n = 0.0, 0
-        for path in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
-            for row in csv.DictReader(open(path)):
-                if "k_render" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                    total += float(row["Counter_Value"])
-                    n += 1
-        shutil.rmtree(out, ignore_errors=True)
-        if n == 0:
-            return None, f"no {ctr} rows for k_render"
-        vals[ctr] = total
-    kb = 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]
-    return kb * 1024.0, {"FETCH_SIZE_KB": vals["FETCH_SIZE"], "WRITE_SIZE_KB": vals["WRITE_SIZE"],
+    try:
+        fetch = _pmc_pass(args, ["FETCH_SIZE"], "fetch")["FETCH_SIZE"]
+        write = _pmc_pass(args, ["WRITE_SIZE"], "write")["WRITE_SIZE"]
+    except RuntimeError as e:
+        return None, str(e)
+    kb = 2.0 * fetch + write
+    return kb * 1024.0, {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
                          "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+
+
+SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU",
+               "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+
+
+def pmc_valu(args, n_cu):
+    """Executed-work view of the render launch (its own --pmc pass): how busy
+    the VALU issue was and how many lanes each VALU instruction had.
+    SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8
+    XCDs (MI355X_MICROARCH.md, cycle constants)."""
+    try:
+        v = _pmc_pass(args, SQ_COUNTERS, "sq")
+    except RuntimeError as e:
+        return {"skipped": str(e)}
+    cycles = v["GRBM_GUI_ACTIVE"] / 8.0
+    simds = 4 * n_cu
+    return {"valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
+            "valu_lane_util": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
+            "valu_insts_per_simd_cycle": round(v["SQ_INSTS_VALU"] / (simds * cycles), 4),
+            "formula": "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8); "
+                       "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)",
+            "counters": v, "cus": n_cu}
 
 
 def cpu_baseline(args, world, frame, gpu_image, budget_s):
@@ -120,7 +154,11 @@ def cpu_baseline(args, world, frame, gpu_image, budget_s):
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
+    visible = len(os.sched_getaffinity(0))
+    # the box's CPU share: OMP_NUM_THREADS is set to it on the GPU box
+    # (16); sched_getaffinity shows every CPU of the host there
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or visible
+    threads = max(1, min(visible, share))
     H = args.height
     order = [(7 + 37 * k) % H for k in range(H)]  # 37 is coprime to 1080: every row once
     done, t0, mism = [], time.perf_counter(), 0
@@ -142,6 +180,8 @@ def cpu_baseline(args, world, frame, gpu_image, budget_s):
     oracle.render_rows(world, frame, np.array(few, np.uint32), nthreads=1)
     dt1 = time.perf_counter() - t1
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "cores_note": f"threads used = min(CPUs in sched_getaffinity ({visible}), OMP_NUM_THREADS "
+                          f"= the box's CPU share ({share}))",
             "sample": f"{len(done)} full rows (x{args.width} px, spp {args.spp}) of the same frame, "
                       f"spread over the image, fp32 oracle (oracle/rtx_oracle.c), {threads} threads, "
                       f"{dt:.1f} s",
@@ -187,7 +227,11 @@ def main():
 
     world, frame = scene_and_frame(args)
     W, H, T, R = args.width, args.height, args.tile_rows, world_size
-    stream = torch.cuda.current_stream()
+    # One stream for everything of a step: the render (librtx), torch's
+    # buffer fills, the RCCL gather (it waits on the current stream) and the
+    # de-interleave all order on it.
+    stream = torch.cuda.Stream(device=local_rank)
+    torch.cuda.set_stream(stream)
     ctx = rtx.Context(local_rank, stream=stream.cuda_stream)
     ctx.upload_world(world)
     ctx.set_frame(frame)
@@ -238,9 +282,10 @@ def main():
         achieved = flops / (launch_ms * 1e-3) / 1e12
         rows0 = rtx.part_rows(H, T, 0, R) if R > 1 else H
         alg_bytes = rows0 * W * 16 + world.count * 32  # framebuffer + scene
-        traffic, pmc_note = (None, "skipped")
+        traffic, pmc_note, executed = (None, "skipped", None)
         if args.pmc == "auto" and R == 1:
             traffic, pmc_note = pmc_traffic(args)
+            executed = pmc_valu(args, torch.cuda.get_device_properties(local_rank).multi_processor_count)
         host_img = image.cpu().numpy() if R == 1 else None
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
@@ -263,7 +308,7 @@ def main():
                        "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                        "spheres": world.count, "rng": args.rng, "tile_rows": T,
                        "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if R > 1 else "")},
-            "roofline": {"bound": "mfma", "roof": "fp32 vector ALU (157.3 TF = fp32 MFMA peak)",
+            "roofline": {"bound": "fp32-valu", "roof": "fp32 vector ALU, 157.3 TF (the kernel issues no MFMA)",
                          "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                          "traffic": None if traffic is None else round(traffic),
@@ -274,7 +319,8 @@ def main():
                          "kernel_ms": round(launch_ms, 4),
                          "flop_per_launch": flops, "sphere_tests_per_launch": tests_per_launch,
                          "segments_per_sample": round(st.segments / max(1, st.samples), 4),
-                         "pmc": pmc_note},
+                         "pmc": pmc_note,
+                         "executed": executed},
             "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(alg_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),

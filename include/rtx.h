@@ -134,8 +134,12 @@ RTX_API int rtx_device_count(int *count);
 RTX_API int rtx_create(int hip_device, rtx_ctx **out);
 RTX_API void rtx_destroy(rtx_ctx *ctx);
 /* Use an external hipStream_t (e.g. torch's current stream) for every later
- * launch; NULL restores the context's own stream. */
+ * launch and copy. NULL is HIP's null (legacy default) stream — the handle
+ * torch reports for its default stream — so that work orders with the
+ * caller's other work on it. */
 RTX_API int rtx_set_stream(rtx_ctx *ctx, void *hip_stream);
+/* Back to the context's own non-blocking stream (the state after rtx_create). */
+RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
 
 /* ---- scene / frame upload ----------------------------------------------
  * ~ CreateBuffer(WorldDef, IMMUTABLE) (DxCSApp.cpp:393-413). */

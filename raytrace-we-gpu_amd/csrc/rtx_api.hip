@@ -42,6 +42,12 @@ struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
+// Launch timing: a fixed ring of event pairs. When every pair is in use the
+// oldest launch's duration is folded into a running total (waiting for its
+// stop event, long finished in practice), so a host that renders forever
+// without rtx_stats_reset keeps kEventRing pairs, not one per launch.
+constexpr size_t kEventRing = 64;
+
 }  // namespace
 
 struct rtx_ctx {
@@ -64,8 +70,9 @@ struct rtx_ctx {
     // framebuffer
     float4 *d_fb = nullptr;
     size_t fb_pixels = 0;
-    // progressive accumulation (linear sums), sized like the framebuffer
+    // progressive accumulation (linear sums) of accum_pixels pixels
     float4 *d_accum = nullptr;
+    size_t accum_pixels = 0;
     uint32_t accum_frames = 0;
     // measurement
     unsigned long long *d_counters = nullptr;
@@ -74,8 +81,9 @@ struct rtx_ctx {
     // LPT scheduling scratch (persistent kernel): cost + perm per pixel
     uint32_t *d_sched = nullptr;
     size_t sched_pixels = 0;
-    std::vector<EventPair> events;  // one pair per launch since reset
-    size_t events_used = 0;
+    EventPair events[kEventRing];   // ring: [ev_head, ev_head + ev_count) outstanding
+    size_t ev_head = 0, ev_count = 0;
+    double ms_folded = 0.0;         // durations of launches whose pair was recycled
     uint64_t samples = 0;
     uint64_t launches = 0;
     bool n_changed = false;  // world resized since the last rtx_stats_reset
@@ -184,8 +192,8 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipFree(c->d_wave_times);
     (void)hipFree(c->d_sched);
     for (auto &p : c->events) {
-        (void)hipEventDestroy(p.start);
-        (void)hipEventDestroy(p.stop);
+        if (p.start) (void)hipEventDestroy(p.start);
+        if (p.stop) (void)hipEventDestroy(p.stop);
     }
     (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -193,7 +201,13 @@ void rtx_destroy(rtx_ctx *c) {
 
 int rtx_set_stream(rtx_ctx *c, void *s) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_set_stream: null ctx");
-    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    c->stream = reinterpret_cast<hipStream_t>(s);  // NULL: HIP's null stream (torch's default stream)
+    return RTX_OK;
+}
+
+int rtx_use_own_stream(rtx_ctx *c) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_use_own_stream: null ctx");
+    c->stream = c->own_stream;
     return RTX_OK;
 }
 
@@ -328,12 +342,16 @@ int rtx_accumulate(rtx_ctx *c, int reset) {
     int rc = set_device(c);
     if (rc) return rc;
     const size_t px = (size_t)c->frame.width * c->frame.height;
-    if (reset || c->accum_frames == 0 || !c->d_accum || c->fb_pixels != px) {
-        if (!c->d_accum || c->fb_pixels != px) {
+    // a frame of another size restarts the accumulation (the accumulator is
+    // indexed by pixel: it must hold exactly width*height sums)
+    if (reset || c->accum_frames == 0 || !c->d_accum || c->accum_pixels != px) {
+        if (!c->d_accum || c->accum_pixels != px) {
             RTX_HIP(hipStreamSynchronize(c->stream));
             (void)hipFree(c->d_accum);
             c->d_accum = nullptr;
+            c->accum_pixels = 0;
             RTX_HIP(hipMalloc(&c->d_accum, px * sizeof(float4)));
+            c->accum_pixels = px;
         }
         RTX_HIP(hipMemsetAsync(c->d_accum, 0, px * sizeof(float4), c->stream));
         c->accum_frames = 0;
@@ -410,13 +428,18 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     }
     rtx::KParams p = make_params(c, rows, tile_rows, part, nparts, out, accum, accum_frames, frame_index);
 
-    if (c->events_used == c->events.size()) {
-        EventPair ev;
-        RTX_HIP(hipEventCreate(&ev.start));
-        RTX_HIP(hipEventCreate(&ev.stop));
-        c->events.push_back(ev);
+    if (c->ev_count == kEventRing) {  // recycle the oldest pair: fold its duration
+        EventPair &old = c->events[c->ev_head];
+        RTX_HIP(hipEventSynchronize(old.stop));
+        float t = 0.0f;
+        RTX_HIP(hipEventElapsedTime(&t, old.start, old.stop));
+        c->ms_folded += t;
+        c->ev_head = (c->ev_head + 1) % kEventRing;
+        c->ev_count--;
     }
-    EventPair &ev = c->events[c->events_used++];
+    EventPair &ev = c->events[(c->ev_head + c->ev_count) % kEventRing];
+    if (!ev.start) RTX_HIP(hipEventCreate(&ev.start));
+    if (!ev.stop) RTX_HIP(hipEventCreate(&ev.stop));
     RTX_HIP(hipEventRecord(ev.start, c->stream));
     const size_t npix = (size_t)rows * f.width;
     if (c->sched_pixels < npix) {
@@ -438,6 +461,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     hipError_t e = rtx::launch_render(p, sched, c->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_render");
     RTX_HIP(hipEventRecord(ev.stop, c->stream));
+    c->ev_count++;
     c->launches++;
     c->samples += (uint64_t)rows * f.width * c->spp;
     return RTX_OK;
@@ -487,7 +511,9 @@ int rtx_stats_reset(rtx_ctx *c) {
     if (rc) return rc;
     RTX_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
-    c->events_used = 0;
+    c->ev_head = 0;
+    c->ev_count = 0;
+    c->ms_folded = 0.0;
     c->samples = 0;
     c->launches = 0;
     c->n_changed = false;
@@ -503,10 +529,11 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     unsigned long long h[4];
     RTX_HIP(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
-    double ms = 0.0;
-    for (size_t i = 0; i < c->events_used; ++i) {
+    double ms = c->ms_folded;
+    for (size_t i = 0; i < c->ev_count; ++i) {
+        const EventPair &p = c->events[(c->ev_head + i) % kEventRing];
         float t = 0.0f;
-        RTX_HIP(hipEventElapsedTime(&t, c->events[i].start, c->events[i].stop));
+        RTX_HIP(hipEventElapsedTime(&t, p.start, p.stop));
         ms += t;
     }
     out->kernel_ms = ms;

@@ -9,8 +9,8 @@ namespace rtx {
 
 // Device scene layout (all in HBM, read-only):
 //   soa   float[n_pad*4]  AoSoA-8 blocks of 8 spheres, 128 B each:
-//                         cx[8] cy[8] cz[8] -(r*r)[8] — streamed by every
-//                         ray segment (LDS broadcast or scalar loads)
+//                         cx[8] cy[8] cz[8] -(r*r)[8] — the exact in-order
+//                         fallback scan (scalar loads)
 //   cen   float4[n]  center.xyz, radius  — read once per hit (normal)
 //   mtype int   [n]  material code 0/1/2, 3 = "no scatter"
 //   mval  float4[n]  albedo.rgb, fuzz-or-ir
@@ -76,21 +76,10 @@ struct KSchedule {
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
 };
-#ifndef RTX_LPT_BUCKETS
-#define RTX_LPT_BUCKETS 256
-#endif
-constexpr uint32_t kCostBuckets = RTX_LPT_BUCKETS;
-#ifndef RTX_LPT_SPP  // pre-pass samples per pixel (kept: the render resumes after them)
-#define RTX_LPT_SPP 2
-#endif
-constexpr uint32_t kCostSpp = RTX_LPT_SPP;
+constexpr uint32_t kCostBuckets = 256;
+constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
 constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
-
-// LDS variant: spheres kept resident in LDS up to this count (16 B each);
-// larger scenes are streamed through LDS in chunks of kChunk spheres.
-constexpr uint32_t kResidentMax = 4096;  // 64 KiB (+ 13 KiB candidate list)
-constexpr uint32_t kChunk = 1024;        // 16 KiB
-constexpr uint32_t kBlock = 256;         // 4 waves
+constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)
 
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream);
 hipError_t launch_cost(const KParams &p, hipStream_t stream);  // exact grid, p.cost_out set

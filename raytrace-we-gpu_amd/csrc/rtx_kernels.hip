@@ -3,29 +3,26 @@
 // (gfx950, wave64) HIP kernel.
 //
 // Design:
-//  * one lane per pixel, exact W x rows grid (the reference over-launches
-//    1024x1024 threads for 1024x576, DxCSApp.cpp:524 — no output difference);
-//  * the reference's RNG chain (one fp32 seed per pixel carried through all
-//    samples, ShaderCompute.hlsl:295,304-309) is kept, and the spp x depth
-//    double loop is flattened into a per-lane state machine: a lane whose
-//    path ends starts its pixel's next sample in the same iteration
-//    ("path regeneration"), so a wave's lanes all trace a segment on every
-//    iteration instead of idling while the longest path of the wave
-//    finishes;
-//  * hit_world is a linear closest-hit scan over the sphere array in index
-//    order (Hittable_list.cpp:3-20 / ShaderCompute.hlsl:188-205) over an
-//    AoSoA-8 layout, so packed-fp32 pairs (v_pk_fma_f32) come straight from
-//    consecutive registers. Sphere data is wave-uniform; RTX_SRC selects
-//    where it is read from: 0 = LDS by broadcast ds_read_b128 (resident for
-//    n <= kResidentMax, streamed in kChunk tiles otherwise), 1 = scalar
-//    loads (s_load into SGPRs through the scalar cache / L2);
-//  * the quadratic's root/sqrt work sits behind the per-sphere "disc >= 0"
-//    branch, so a wave skips it when no lane's ray line meets the sphere
-//    (the wave-level early-out on all-miss);
+//  * chain RNG (the reference, ShaderCompute.hlsl:295,304-309): one lane per
+//    pixel; the spp x depth double loop is flattened into a per-lane state
+//    machine (a lane whose path ends starts its pixel's next sample in the
+//    same iteration), persistent lanes pull pixels from a cost-ordered queue,
+//    and the heaviest pixels are traced by groups of lanes (k_render);
+//  * per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample)
+//    (k_render_ps): samples are independent, so a wave's lanes trace
+//    consecutive samples of a batch of pixels and fold each pixel's sample
+//    colours in sample order afterwards;
+//  * hit_world is a line-distance prefiltered scan over the sphere array
+//    (scalar loads of AoSoA-8 blocks, packed-fp32 pairs, one max + ballot
+//    per 8 spheres = the wave-level early-out on all-miss), then the
+//    flagged spheres are resolved with the reference's own ops
+//    (Hittable_list.cpp:3-20 / ShaderCompute.hlsl:188-205);
 //  * the hit record (p, normal, front_face, material) is built once per
 //    segment for the winning sphere, not for every accepted candidate —
 //    identical values, because the reference's final record is the last
 //    accepted one.
+// Measured-and-rejected variants (LDS-resident spheres, pre-prefilter scans,
+// ...) are in git history and DESIGN.md §7.
 #include "rtx_device_math.h"
 #include "rtx_internal.h"
 #include "rtx_prefilter.h"
@@ -70,16 +67,9 @@ __device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_
 // a = |d|^2 (Sphere.cpp:8; HLSL length(d)*length(d), :160), fma form.
 __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y, d.y, d.x * d.x)); }
 
-#ifndef RTX_SRC
-#define RTX_SRC 1
-#endif
-#ifndef RTX_BATCH
-#define RTX_BATCH 8
-#endif
-static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
-#ifndef RTX_COOP_MAX  // tail mode: a wave with <= this many active lanes traces their rays together
-#define RTX_COOP_MAX 8
-#endif
+// Compile-time knobs. The diagnostics are separate builds (Makefile
+// variants prof/ptime/cprof); the candidate-list capacities below are also
+// set by the stress build. Everything else is a fixed product constant.
 #ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
 #define RTX_DIAG_PROF 0
 #endif
@@ -89,77 +79,24 @@ static_assert(RTX_BATCH == 4 || RTX_BATCH == 8, "RTX_BATCH must be 4 or 8");
 #ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
 #define RTX_DIAG_COOP 0
 #endif
-#ifndef RTX_SHADE_MERGE  // 1: Lambert and metal lanes share one scatter path
-#define RTX_SHADE_MERGE 1
-#endif
-#ifndef RTX_PERSISTENT  // 1: lanes pull pixels from a cost-ordered queue; 0: one pixel per lane
-#define RTX_PERSISTENT 1
-#endif
-#ifndef RTX_PRETEST  // 1: skip roots of spheres entirely behind the ray (exact, see below)
-#define RTX_PRETEST 0
-#endif
-#ifndef RTX_ANYMAX  // 1: all-miss test on max(disc) instead of one ballot per sphere
-#define RTX_ANYMAX 1
-#endif
-#ifndef RTX_DIAG_NOBRANCH  // timing-only diagnostic: never compute roots (WRONG images)
-#define RTX_DIAG_NOBRANCH 0
-#endif
-#ifndef RTX_DEFER  // 1: record candidates during the scan, resolve them afterwards
-#define RTX_DEFER 1
-#endif
-#ifndef RTX_LISTMASK  // 1: one list entry per 4-sphere batch (index | 4-bit mask << 28)
-#define RTX_LISTMASK 1
-#endif
-#ifndef RTX_PREFILTER  // 1: scan with the line-distance prefilter (rtx_prefilter.h; RTX_SRC 1 only)
-#define RTX_PREFILTER 1
-#endif
-#ifndef RTX_HEAVY_WAVE  // heavy pixels per group-coop wave (0: no heavy split)
-#define RTX_HEAVY_WAVE 8
-#endif
-#ifndef RTX_HEAVY_ALPHA  // heavy iff key > alpha * (a lane's share of the summed keys)
-#define RTX_HEAVY_ALPHA 2.0
-#endif
-#ifndef RTX_PRIO_FRAC_X100  // hot-wave priority: prio_slots = this % of the resident lanes (0 = off)
-#define RTX_PRIO_FRAC_X100 20
-#endif
-#ifndef RTX_TAIL_PRIO  // wave priority of a normal wave in its coop tail
-#define RTX_TAIL_PRIO 1
-#endif
-#ifndef RTX_HEAVY_RHO  // "small" frame share: fewer pixels than rho * resident lanes
-#define RTX_HEAVY_RHO 1.2
-#endif
-#ifndef RTX_HEAVY_RHO2  // "medium" frame share: fewer pixels than rho2 * resident lanes (0 = off)
-#define RTX_HEAVY_RHO2 3.5
-#endif
-#ifndef RTX_HEAVY2_ALPHA_MEDIUM  // tier 2 for a medium share: key > this * share
-#define RTX_HEAVY2_ALPHA_MEDIUM 1.5
-#endif
-#ifndef RTX_HEAVY1_ALPHA  // tier 1 iff key > alpha1 * a lane's share of the summed keys
-#define RTX_HEAVY1_ALPHA 1.7
-#endif
-#ifndef RTX_HEAVY1_ALPHA_SMALL  // the same for a small frame share
-#define RTX_HEAVY1_ALPHA_SMALL 4.0
-#endif
-#ifndef RTX_HEAVY1_WAVE  // tier-1 heavy pixels per wave
-#define RTX_HEAVY1_WAVE 1
-#endif
-#ifndef RTX_BLOCK  // threads per render workgroup (64 = one wave: freed slots refill independently)
-#define RTX_BLOCK 256
-#endif
-constexpr uint32_t kRB = RTX_BLOCK;
-static_assert(kRB % 64 == 0 && kRB <= 1024, "RTX_BLOCK must be a multiple of 64");
-#ifndef RTX_WAVES_PER_SIMD  // occupancy request for the render kernels (0 = compiler's choice)
-#define RTX_WAVES_PER_SIMD 5  // 96 VGPRs (the compiler's own choice is 100: 4 waves); the
-                              // few spills (SGPRs to VGPR lanes, ~7 VGPR dwords to scratch) sit in
-                              // per-segment and coop code, none in the lane-mode scan loop
-#endif
-#if RTX_WAVES_PER_SIMD
+constexpr int kCoopMax = 8;             // tail mode: a wave with <= this many active lanes traces their rays together
+constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wave
+constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
+constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha * a lane's share of the summed keys
+constexpr double kHeavy1Alpha = 1.7;    // tier 1 iff key > alpha1 * share
+constexpr double kHeavy1AlphaSmall = 4.0;   // the same for a small frame share
+constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
+constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
+constexpr double kHeavy2AlphaMedium = 1.5;  // tier 2 for a medium share: key > this * share
+constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
+constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
+constexpr uint32_t kRB = 256;           // threads per render workgroup
+#define RTX_WAVES_PER_SIMD 5  // occupancy request for the render kernels: 96 VGPRs (the compiler's own
+                              // choice is 100: 4 waves); the few spills (SGPRs to VGPR lanes, ~7 VGPR
+                              // dwords to scratch) sit in per-segment and coop code, none in the scan loop
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
-#else
-#define RTX_RENDER_BOUNDS __launch_bounds__(kRB)
-#endif
 
-// Candidate list (RTX_DEFER): per lane kCand slots in LDS, slot-major
+// Candidate list: per lane kCand slots in LDS, slot-major
 // (slot j of lane t at [j * kRB + t]: conflict-free), plus one dump slot
 // that absorbs writes past the end (the lane then falls back, see below).
 #ifndef RTX_CAND  // candidate-list capacity per lane (entries; a full list is resolved in rounds)
@@ -218,229 +155,48 @@ __device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, 
 // One ray against `nblk` AoSoA-8 blocks (global sphere index of block b's
 // first sphere: 8 * (blk0 + b)), in index order; `best` is closest_so_far
 // (t_max shrinks on every accepted hit, :196-200). Returns the winning
-// index or `idx`.
+// index or `idx`. This is the exact fallback of the prefiltered hit_world
+// (a lane with a non-finite root redoes the range with it).
 //
 // Per sphere ("hit_sphere"): oc = o - c; hb = oc.d;
 // cc = |oc|^2 - r^2; disc = hb^2 - a*cc. NaN disc falls through like the
-// reference's `if (d < 0) return false`. RTX_BATCH spheres per step: their
-// reads issue together and one wave-uniform branch skips the root work
-// when no lane's ray line meets any of them (all-miss early out).
+// reference's `if (d < 0) return false`. 8 spheres per step: their reads
+// issue together and one wave-uniform branch skips the root work when no
+// lane's ray line meets any of them (all-miss early out).
 template <typename Ptr>
 __device__ __forceinline__ int hit_blocks_seq(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d,
                                               float a, float inv_a, float t_min, float &best,
                                               int idx) {
     for (uint32_t b = 0; b < nblk; ++b) {
         const Ptr blk = soa + 32 * b;
+        float hb[8], disc[8];
 #pragma unroll
-        for (int h = 0; h < 8; h += RTX_BATCH) {
-            float cx[RTX_BATCH], cy[RTX_BATCH], cz[RTX_BATCH], nr2[RTX_BATCH];
+        for (int k = 0; k < 8; ++k) {
+            const float ocx = o.x - blk[k];
+            const float ocy = o.y - blk[8 + k];
+            const float ocz = o.z - blk[16 + k];
+            hb[k] = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
+            const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + k])));
+            disc[k] = fmaf(hb[k], hb[k], -(a * cc));
+        }
+        // max() drops a NaN operand: a batch mixing NaN and negative discs
+        // needs an fp32 overflow in hb^2 or a*cc, which rtx_upload_world's
+        // bound (|scene values| <= 1e15) rules out; an all-NaN batch (NaN
+        // ray) yields NaN and is taken, like the reference.
+        float m = disc[0];
 #pragma unroll
-            for (int q = 0; q < RTX_BATCH; ++q) {
-                cx[q] = blk[h + q];
-                cy[q] = blk[8 + h + q];
-                cz[q] = blk[16 + h + q];
-                nr2[q] = blk[24 + h + q];
-            }
-            float hb[RTX_BATCH], disc[RTX_BATCH], cc[RTX_BATCH];
-            uint64_t any = 0;
+        for (int k = 1; k < 8; ++k) m = fmaxf(m, disc[k]);
+        if (__ballot(!(m < 0.0f)) != 0ull) {
+            const int g = (int)(8 * (blk0 + b));
 #pragma unroll
-            for (int k = 0; k < RTX_BATCH; ++k) {
-                const float ocx = o.x - cx[k];
-                const float ocy = o.y - cy[k];
-                const float ocz = o.z - cz[k];
-                hb[k] = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-                cc[k] = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, nr2[k])));
-                disc[k] = fmaf(hb[k], hb[k], -(a * cc[k]));
-#if !RTX_ANYMAX
-                any |= __ballot(!(disc[k] < 0.0f));
-#endif
-            }
-#if RTX_ANYMAX
-            // max() drops a NaN operand: a batch mixing NaN and negative discs
-            // needs an fp32 overflow in hb^2 or a*cc, which rtx_upload_world's
-            // bound (|scene values| <= 1e15) rules out; an all-NaN batch (NaN
-            // ray) yields NaN and is taken, like the reference.
-            float m = disc[0];
-#pragma unroll
-            for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
-            any = __ballot(!(m < 0.0f));
-#endif
-#if RTX_DIAG_NOBRANCH
-#pragma unroll
-            for (int k = 0; k < RTX_BATCH; ++k) asm volatile("" ::"v"(disc[k]), "v"(hb[k]));
-            (void)any;
-#else
-            if (any != 0ull) {
-                const int g = (int)(8 * (blk0 + b) + h);
-#pragma unroll
-                for (int k = 0; k < RTX_BATCH; ++k) {
-#if RTX_PRETEST
-                    // Sphere ahead of the origin? If hb > 0 and cc > 0 (origin
-                    // outside, moving away) both fp32 roots are < 0 <= t_min:
-                    // -hb - s < 0, and s = RN(sqrt(RN(hb^2 - x))) <= hb for
-                    // x = RN(a*cc) >= 0 because sqrt(RN(hb^2)) == hb when hb^2
-                    // is a normal number (1e-15 < hb < 1e18).
-                    const bool behind = hb[k] > 1e-15f && hb[k] < 1e18f && cc[k] > 0.0f;
-                    if (!(disc[k] < 0.0f) && !behind)
-#else
-                    if (!(disc[k] < 0.0f))
-#endif
-                        sphere_roots(hb[k], disc[k], inv_a, t_min, best, idx, g + k);
-                }
-            }
-#endif
+            for (int k = 0; k < 8; ++k)
+                if (!(disc[k] < 0.0f)) sphere_roots(hb[k], disc[k], inv_a, t_min, best, idx, g + k);
         }
     }
     return idx;
 }
 
 typedef const __attribute__((address_space(4))) float *cfloat_p;  // constant AS: scalar loads
-
-// ---- deferred candidate resolution ----------------------------------------
-// The sequential scan above accepts sphere i iff its candidate root
-//   c_i = rn if rn >= t_min, else rf if rf >= t_min, else none
-// satisfies c_i <= B_i, the running best (t_max initially) — rn > B_i makes
-// rf >= rn > B_i too, since s >= 0 and multiplying by inv_a > 0 is monotone
-// in fp32. c_i does not depend on B_i, so for finite roots the result is
-// (min c_i, largest index among the minima), in ANY evaluation order. The
-// scan therefore only records the spheres whose disc >= 0 (or NaN) in a
-// per-lane list and resolves them afterwards with all lanes working on
-// their own candidates at once, instead of running the sqrt/root code for
-// each sphere under the one or two lanes that need it. A lane with more
-// than kCand candidates, or any non-finite root (NaN/zero-length ray,
-// overflow), redoes the range with the exact sequential scan.
-template <typename Ptr>
-__device__ __forceinline__ uint32_t scan_candidates(Ptr soa, uint32_t nblk, f3 o, f3 d, float a,
-                                                    uint32_t *list) {
-    uint32_t cnt = 0;
-    uint32_t *my = list + threadIdx.x;
-    for (uint32_t b = 0; b < nblk; ++b) {
-        const Ptr blk = soa + 32 * b;
-#pragma unroll
-        for (int h = 0; h < 8; h += RTX_BATCH) {
-            float disc[RTX_BATCH];
-            uint64_t any = 0;
-#pragma unroll
-            for (int k = 0; k < RTX_BATCH; ++k) {
-                const float ocx = o.x - blk[h + k];
-                const float ocy = o.y - blk[8 + h + k];
-                const float ocz = o.z - blk[16 + h + k];
-                const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-                const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + h + k])));
-                disc[k] = fmaf(hb, hb, -(a * cc));
-#if !RTX_ANYMAX
-                any |= __ballot(!(disc[k] < 0.0f));
-#endif
-            }
-#if RTX_ANYMAX
-            float m = disc[0];
-#pragma unroll
-            for (int k = 1; k < RTX_BATCH; ++k) m = fmaxf(m, disc[k]);
-            any = __ballot(!(m < 0.0f));
-#endif
-            RTX_DIAG_ADD(0, 1u);
-            if (any != 0ull) {
-                RTX_DIAG_ADD(1, 1u);
-#if RTX_LISTMASK
-#pragma unroll
-                for (int q = 0; q < RTX_BATCH; q += 4) {
-                    const uint32_t m = (!(disc[q] < 0.0f) ? 1u : 0u) | (!(disc[q + 1] < 0.0f) ? 2u : 0u) |
-                                       (!(disc[q + 2] < 0.0f) ? 4u : 0u) | (!(disc[q + 3] < 0.0f) ? 8u : 0u);
-                    my[min(cnt, (uint32_t)kCand) * kRB] = (8 * b + h + q) | (m << 28);
-                    cnt += m != 0u ? 1u : 0u;
-                }
-#else
-#pragma unroll
-                for (int k = 0; k < RTX_BATCH; ++k) {
-                    // write unconditionally at the next free slot (or the
-                    // dump slot), advance only for a candidate
-                    my[min(cnt, (uint32_t)kCand) * kRB] = 8 * b + h + k;
-                    cnt += !(disc[k] < 0.0f) ? 1u : 0u;
-                }
-#endif
-            }
-        }
-    }
-    return cnt;
-}
-
-// Resolve the lane's candidates (local indices into `soa`, global index =
-// 8*blk0 + local). List entries are `first local index | mask << kSh`.
-// A candidate whose exact disc is < 0 (a prefilter false positive) is
-// skipped, as the reference's `if (d < 0) return false`. Returns false if
-// the lane must fall back.
-template <int kSh, typename Ptr>
-__device__ __forceinline__ bool resolve_candidates(Ptr soa, uint32_t blk0, const uint32_t *list,
-                                                   uint32_t cnt, f3 o, f3 d, float a, float inv_a,
-                                                   float t_min, float &best, int &idx) {
-    bool ok = cnt <= (uint32_t)kCand;
-    const uint32_t m = ok ? cnt : 0u;
-    const float inf = __uint_as_float(0x7f800000u);
-#if RTX_LISTMASK
-    uint32_t j = 0, e = 0;  // entry index, remaining mask bits of entry j
-    if (m) e = list[threadIdx.x];
-    RTX_DIAG_ADD(4, (uint32_t)__popcll(__ballot(m != 0u)));
-    for (;;) {
-        const bool live = j < m;
-        if (__ballot(live) == 0ull) break;
-        RTX_DIAG_ADD(2, 1u);
-        if (live) {
-            const uint32_t k = (uint32_t)__builtin_ctz(e >> kSh);
-            const uint32_t i = (e & ((1u << kSh) - 1u)) + k;
-            e &= ~(1u << (kSh + k));
-            if ((e >> kSh) == 0u && ++j < m) e = list[j * kRB + threadIdx.x];
-#else
-    for (uint32_t j = 0; __ballot(j < m) != 0ull; ++j) {
-        if (j < m) {
-            const uint32_t i = list[j * kRB + threadIdx.x];
-#endif
-            const Ptr blk = soa + 32 * (i >> 3);
-            const uint32_t q = i & 7u;
-            const float ocx = o.x - blk[q];
-            const float ocy = o.y - blk[8 + q];
-            const float ocz = o.z - blk[16 + q];
-            const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
-            const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, blk[24 + q])));
-            const float disc = fmaf(hb, hb, -(a * cc));
-            if (!(disc < 0.0f)) {
-                const float sq = sqrtf(disc);
-                const float rn = (-hb - sq) * inv_a;
-                const float rf = (-hb + sq) * inv_a;
-                if (!(fabsf(rn) < inf) || !(fabsf(rf) < inf)) ok = false;
-                const bool use_n = !(rn < t_min);
-                const float c = use_n ? rn : rf;
-                const int g = (int)(8 * blk0 + i);
-                if ((use_n || !(rf < t_min)) && (c < best || (c == best && g > idx))) {
-                    best = c;
-                    idx = g;
-                }
-            }
-        }
-    }
-    return ok;
-}
-
-// hit_world over nblk sphere blocks (global block offset blk0), updating
-// (best, idx) exactly as the reference's in-order scan would.
-template <typename Ptr>
-__device__ __forceinline__ int hit_world(Ptr soa, uint32_t nblk, uint32_t blk0, f3 o, f3 d, float a,
-                                         float inv_a, float t_min, float &best, int idx,
-                                         uint32_t *list) {
-#if RTX_DEFER && !RTX_DIAG_NOBRANCH
-    const float best0 = best;
-    const int idx0 = idx;
-    const uint32_t cnt = scan_candidates(soa, nblk, o, d, a, list);
-    if (!resolve_candidates<28>(soa, blk0, list, cnt, o, d, a, inv_a, t_min, best, idx)) {
-        RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
-        best = best0;
-        idx = hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx0);
-    }
-    return idx;
-#else
-    (void)list;
-    return hit_blocks_seq(soa, nblk, blk0, o, d, a, inv_a, t_min, best, idx);
-#endif
-}
 
 // ---- prefiltered scan (rtx_prefilter.h) -----------------------------------
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -454,7 +210,7 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // Returns the block to resume at: nblk, or earlier once some lane's list is
 // full (kCand entries) and must be resolved first (wave-uniform).
 //
-// RTX_SCAN_PF 1: the block's 32 floats are double-buffered in SGPRs. The
+// kPF (scenes above kScanPfMin): the block's 32 floats are double-buffered in SGPRs. The
 // next block's two s_load_dwordx16 are issued (inline asm: the compiler
 // otherwise sinks them to the end of the iteration and waits at once) before
 // this block's 33 VALU instructions and waited for after them, so a scalar
@@ -462,12 +218,6 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
 // loaded registers ("+s") so that nothing reads them before it. Every path
 // out of the loop body passes a wait, so no load is in flight at exit.
-#ifndef RTX_RESOLVE_LDS  // 1: lane-mode resolve reads sphere data from the block's LDS copy (small scenes)
-#define RTX_RESOLVE_LDS 1
-#endif
-#ifndef RTX_SCAN_PF  // 0: no kPF kernels (every scene takes the plain scan)
-#define RTX_SCAN_PF 1
-#endif
 constexpr uint32_t kScanPfMin = 1024;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
 typedef float f16v __attribute__((ext_vector_type(16)));
 // Issue block p's loads; the "+v" operands (the line's basis, which every
@@ -619,7 +369,7 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // order-independent, so rounds compose. A non-finite root takes
 // hit_blocks_seq.
 // `ld(i)` returns (center, radius) of sphere i for the resolve (cen in HBM,
-// or the block's LDS copy of the coop's sphere data, RTX_RESOLVE_LDS).
+// or, for scenes up to kCoopLds spheres, the block's LDS copy of them).
 template <bool kPF, typename Ld>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
                                                 float t_min, float &best, uint32_t *list) {
@@ -649,21 +399,9 @@ __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float 
     return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list);
 }
 
-// One ray segment against the whole scene with sphere data read through
-// scalar loads (RTX_SRC 1 and the debug kernel).
-template <bool kPF = false>
-__device__ __forceinline__ int trace_scalar(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
-                                            float &best, uint32_t *list) {
-#if RTX_PREFILTER
-    return hit_world_pre<kPF>(S, o, d, a, inv_a, t_min, best, list);
-#else
-    return hit_world((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1, list);
-#endif
-}
-
 // ---- group-cooperative hit_world (frame tail) ------------------------------
 // Once the pixel queue is empty a wave runs on until its last pixel ends,
-// and the frame ends on the most expensive pixels. With m <= RTX_COOP_MAX
+// and the frame ends on the most expensive pixels. With m <= kCoopMax
 // rays left, the wave traces them together: ray r (the r-th active lane)
 // by the g = 64 / 2^ceil(log2 m) lanes [r*g, r*g + g). Lane k of a group
 // runs the prefilter over spheres k, k+g, ... (pre4), resolves what it
@@ -675,19 +413,9 @@ __device__ __forceinline__ int trace_scalar(const KScene &S, f3 o, f3 d, float a
 constexpr uint32_t kCoopSlots = 32;                                   // rays per wave in coop mode
 constexpr uint32_t kCoopWaveBytes = kCoopSlots * 10 * sizeof(float);  // ray (8 floats) + 64-bit key
 constexpr uint32_t kCoopBytes = (kRB / 64) * kCoopWaveBytes;
-#ifndef RTX_COOP_STEP
-#define RTX_COOP_STEP 2
-#endif
-constexpr uint32_t kCoopStep = RTX_COOP_STEP;
-#ifndef RTX_ONE_DEFER  // one-ray coop: flag a window, then resolve (1) / resolve on the spot (0)
-#define RTX_ONE_DEFER 0  // 1 measured no better
-#endif
-#ifndef RTX_ONE_STEP  // one-ray coop, deferred: spheres per scan step (reads in flight)
-#define RTX_ONE_STEP 4
-#endif
-[[maybe_unused]] constexpr uint32_t kOneStep = RTX_ONE_STEP;  // spheres per coop step (reads in flight)
+constexpr uint32_t kCoopStep = 2;  // spheres per coop scan step (reads in flight)
 constexpr uint32_t kCoopLds = 704;  // scenes up to this many spheres keep pre4 + radii in LDS for the coop (<= 13.75 KiB: 5 blocks/CU)
-static_assert(RTX_COOP_MAX <= (int)kCoopSlots, "RTX_COOP_MAX must be <= 32");
+static_assert(kCoopMax <= (int)kCoopSlots, "kCoopMax must be <= 32");
 
 // Reduction over aligned groups of 2^lg lanes (lg wave-uniform, whole wave
 // active): DPP inside a row of 16 (quad_perm xor 1 and xor 2, then the
@@ -779,38 +507,6 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
         const f3 ro = mk3(read_lane(w[0], 0), read_lane(w[1], 0), read_lane(w[2], 0));
         const f3 rd = mk3(read_lane(w[3], 0), read_lane(w[4], 0), read_lane(w[5], 0));
         const float ra = read_lane(w[6], 0), ria = read_lane(w[7], 0);
-#if RTX_ONE_DEFER
-        // windows of up to 32 spheres per lane: scan the window (kOneStep
-        // reads in flight) into a flag mask, then resolve the flags, one per
-        // lane per pass, so the wave pays one resolve latency per pass
-        // rather than one per scan step in which any lane flagged
-        for (;;) {
-            if (__ballot(i < i1) == 0ull) break;
-            const uint32_t w0 = i, we = min(i1, w0 + 32u);
-            uint32_t fm = 0;
-            for (;;) {
-                const bool more = i < we;
-                if (__ballot(more) == 0ull) break;
-                float4 pq[kOneStep];
-#pragma unroll
-                for (uint32_t u = 0; u < kOneStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
-#pragma unroll
-                for (uint32_t u = 0; u < kOneStep; ++u)
-                    if (i + u < we && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr))
-                        fm |= 1u << (i + u - w0);
-                i = more ? i + kOneStep : i;
-            }
-            i = w0 < i1 ? we : w0;
-            while (__ballot(fm != 0u) != 0ull) {
-                const bool live = fm != 0u;
-                const uint32_t j = min(w0 + (uint32_t)__builtin_ctz(live ? fm : 1u), n - 1u);
-                fm &= fm - 1u;
-                const float4 pj = sph4[j];
-                const float rr = rad ? rad[j] : S.cen[j].w;
-                resolve_one(make_float4(pj.x, pj.y, pj.z, rr), (int)j, live, ro, rd, ra, ria, t_min, bc, bg, ok);
-            }
-        }
-#else
         for (;;) {
             const bool more = i < i1;
             if (__ballot(more) == 0ull) break;
@@ -828,7 +524,6 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
             }
             i = more ? i + kCoopStep : i;
         }
-#endif
     } else do {
         uint32_t cnt = 0;
         for (;;) {
@@ -920,13 +615,11 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
 // unsafe line flags every sphere), sends the ray (the wave's rays) to the
 // exact sequential path. LDS per wave (coop_ws, 1280 B): rays [8][8] floats,
 // lines [8][8], keys [8] u64, bad [8], count, pairs [kSmCand].
-#ifndef RTX_COOP_SM  // multi-ray coop waves with at least this many rays use groups_sm (0 = never)
-#define RTX_COOP_SM 4
-#endif
+constexpr int kCoopSm = 4;  // multi-ray coop waves with at least this many rays use groups_sm
 #ifndef RTX_SM_CAND  // sphere-major coop: (sphere, ray) pairs per wave before the exact fallback
 #define RTX_SM_CAND 160
 #endif
-[[maybe_unused]] constexpr uint32_t kSmRays = 8, kSmCand = RTX_SM_CAND;
+constexpr uint32_t kSmRays = 8, kSmCand = RTX_SM_CAND;
 static_assert((160 + kSmCand) * sizeof(float) <= kCoopWaveBytes, "sphere-major coop LDS");
 template <typename Q4>
 __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,
@@ -1046,13 +739,11 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, const 
                                                 unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
     if (__popcll(act) == 1)
         return groups_impl<true>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
-#if RTX_COOP_SM
-    static_assert(RTX_COOP_MAX <= (int)kSmRays && RTX_HEAVY_WAVE <= (int)kSmRays, "coop waves hold <= 8 rays");
+    static_assert(kCoopMax <= (int)kSmRays && kHeavy2 <= kSmRays, "coop waves hold <= 8 rays");
     // 2-3 rays: groups of 32 or 16 lanes scan short chunks; from 4 rays on
     // (chunks of 31+ spheres per lane) the sphere-major pass is faster
-    if (__popcll(act) >= RTX_COOP_SM)
+    if (__popcll(act) >= kCoopSm)
         return groups_sm(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, best, seq, cp, tq);
-#endif
     return groups_impl<false>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
 }
 
@@ -1151,9 +842,8 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
         const float4 mv = S.mval[hit];
         f3 dir;
         bool scattered = true;
-#if RTX_SHADE_MERGE
         // Lambert and metal share random_in_unit_sphere and normalize: run
-        // them once for both kinds of lane (same ops per lane as below).
+        // them once for both kinds of lane (each lane's ops are the HLSL's).
         if (mt == 0 || mt == 1) {
             const f3 rius = random_in_unit_sphere(L.seed);
             const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
@@ -1161,19 +851,6 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
             dir = normalize3(lambert_guard(v, nrm, mt == 0 && (P.flags & kFrameLambertGuard) != 0u));
             L.col = L.col * mk3(mv.x, mv.y, mv.z);
         } else if (mt == 2) {
-#else
-        if (mt == 0) {  // DIFFUSE (:209-217)
-            const f3 rius = random_in_unit_sphere(L.seed);
-            const f3 target = (p + nrm) + rius;
-            dir = normalize3(lambert_guard(target - p, nrm, (P.flags & kFrameLambertGuard) != 0u));
-            L.col = L.col * mk3(mv.x, mv.y, mv.z);
-        } else if (mt == 1) {  // METAL (:219-227), always scatters
-            const f3 refl = reflect3(L.d, nrm);
-            const f3 rius = random_in_unit_sphere(L.seed);
-            dir = normalize3(refl + mv.w * rius);
-            L.col = L.col * mk3(mv.x, mv.y, mv.z);
-        } else if (mt == 2) {
-#endif
             // DIELECTRIC (:229-249), atten = 1
             const float ratio = ff ? (1.0f / mv.w) : mv.w;
             const f3 ud = normalize3(L.d);
@@ -1302,8 +979,6 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // segment); tier 2 = slots [k1, kh), up to kHeavy2 per wave. An idle wave
 // tries tier 1 first; a tier-2 wave tops itself up from tier 2. Returns the
 // wave's tier (0: not heavy any more).
-constexpr uint32_t kHeavy1 = RTX_HEAVY1_WAVE;
-constexpr uint32_t kHeavy2 = RTX_HEAVY_WAVE;
 struct HeavyState {
     uint32_t k1, kh;     // tier ends
     bool t1_done, t2_done;
@@ -1344,21 +1019,20 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
         H.tier = 2;
 }
 
-// Render kernel, per-wave independent: RTX_SRC 0 keeps the sphere blocks
-// resident in LDS (one copy per workgroup), 1 reads them with scalar loads.
-// kPersist: the grid holds as many waves as the GPU keeps resident and
+// Render kernel (chain RNG), per-wave independent; sphere blocks are read
+// with scalar loads (a block-wide LDS copy serves the coop and the resolve of
+// scenes up to kCoopLds spheres). kPersist: the grid holds as many waves as the GPU keeps resident and
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
 template <bool kPersist, bool kCost = false, bool kPF = false>
 __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
-    // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][sphere data (coop LDS copy / RTX_SRC 0)]
+    // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][coop LDS copy of the spheres]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
     constexpr uint32_t kLB = list_bytes<kPF>();
     float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
     (void)coop_ws;
-#if RTX_SRC == 1
     // the coop's sphere data: a block-wide LDS copy of pre4 for small scenes
     float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
     float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
@@ -1370,16 +1044,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         }
         __syncthreads();
     }
-#endif
     const int last = (int)P.scene.n - 1;
-#if RTX_SRC == 0
-    const uint32_t nblk = P.scene.n_pad / 8;
-    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
-    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
-    const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
-    for (uint32_t i = threadIdx.x; i < 8 * nblk; i += kRB) s_blk4[i] = g4[i];
-    __syncthreads();
-#endif
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
     const unsigned long long t_start = P.wave_times ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1435,8 +1100,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         pr[4]++;
         pr[6] += __popcll(act);
 #endif
-#if RTX_SRC == 1
-        if (heavy || (RTX_COOP_MAX && exhausted && __popcll(act) <= RTX_COOP_MAX)) {
+        if (heavy || (exhausted && __popcll(act) <= kCoopMax)) {
 #if RTX_DIAG_PROF
             pr[5]++;
 #endif
@@ -1450,7 +1114,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             else if (H.tier == 2u)
                 __builtin_amdgcn_s_setprio(2);
             else
-                __builtin_amdgcn_s_setprio(RTX_TAIL_PRIO);
+                __builtin_amdgcn_s_setprio(kTailPrio);
 #if RTX_DIAG_COOP
             unsigned long long *cp = H.tier == (uint32_t)RTX_DIAG_COOP ? cpa : nullptr;
             unsigned long long *ctqp = &ctq;
@@ -1472,7 +1136,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
-                    my_hit = trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
+                    my_hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
                 shade<kCost>(P, F, L, min(my_hit, last), my_best);
             }
@@ -1488,8 +1152,6 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             RTX_PROF(3)
             continue;
         }
-#endif
-#if RTX_PRIO_FRAC_X100
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
@@ -1497,12 +1159,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             __builtin_amdgcn_s_setprio(3);
         else
             __builtin_amdgcn_s_setprio(0);
-#endif
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
-#if RTX_SRC == 0
-            const int hit = hit_world(s_blk, nblk, 0, L.o, L.d, L.a, L.inv_a, kTMin, best, -1, list);
-#elif RTX_PREFILTER && RTX_RESOLVE_LDS
             // scenes that fit the coop's LDS copy resolve their candidates
             // from it (same centre floats, cen.w = s_rad) instead of HBM/L2
             const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
@@ -1512,10 +1170,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                             return make_float4(c.x, c.y, c.z, s_rad[i]);
                                                         },
                                                         L.o, L.d, L.a, L.inv_a, kTMin, best, list)
-                                : trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
-#else
-            const int hit = trace_scalar<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
-#endif
+                                : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             RTX_PROF(1)
             shade<kCost>(P, F, L, min(hit, last), best);
         }
@@ -1539,70 +1194,23 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     }
 }
 
-// Large scenes with RTX_SRC 0: every ray segment streams the sphere blocks
-// through LDS in kChunk-sphere tiles shared by the block's 4 waves
-// (block-synchronous; the pixel queue is still per wave).
-__global__ void RTX_RENDER_BOUNDS k_render_streamed(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
-    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    float4 *s_blk4 = reinterpret_cast<float4 *>(s_mem + kListBytes);
-    const float *s_blk = reinterpret_cast<const float *>(s_blk4);
-    const uint32_t nblk = P.scene.n_pad / 8;
-    const int last = (int)P.scene.n - 1;
-    const float4 *g4 = reinterpret_cast<const float4 *>(P.scene.soa);
-    const Frame F = load_frame(P);
-    const uint32_t npix = P.rows_local * P.width;
-    Lane L;
-    L.active = false;
-    L.segs = 0;
-    bool exhausted = false;
-    constexpr uint32_t kChunkBlk = kChunk / 8;
-    for (;;) {
-        if (!exhausted) exhausted = refill(P, F, 0, npix, L);
-        if (!__syncthreads_or(L.active ? 1 : 0)) break;
-        float best = __uint_as_float(0x7f800000u);
-        int hit = -1;
-        for (uint32_t b0 = 0; b0 < nblk; b0 += kChunkBlk) {
-            const uint32_t cnt = min(kChunkBlk, nblk - b0);
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < 8 * cnt; i += kRB) s_blk4[i] = g4[8 * b0 + i];
-            __syncthreads();
-            if (L.active) hit = hit_world(s_blk, cnt, b0, L.o, L.d, L.a, L.inv_a, kTMin, best, hit, list);
-        }
-        if (L.active) shade(P, F, L, min(hit, last), best);
-    }
-    count_segments(P, L.segs);
-}
-
 // ---- cost-ordered pixel queue (LPT scheduling, see KSchedule) ------------
 // One sample's segment count is a noisy estimate of a pixel's cost; the
 // key is the sum over a (2R+1)^2 window of neighbouring pixels (clamped
 // at the edges), which averages that noise over similar pixels.
-#ifndef RTX_LPT_RADIUS
-#define RTX_LPT_RADIUS 1
-#endif
-#ifndef RTX_LPT_PERSIST_PREPASS  // 1: the cost pre-pass runs on persistent lanes (index order; measured ~1 % slower)
-#define RTX_LPT_PERSIST_PREPASS 0
-#endif
-#ifndef RTX_LPT_RESUME  // 1: the render resumes each pixel after the pre-pass's samples
-#define RTX_LPT_RESUME 1
-#endif
-#ifndef RTX_LPT_CW  // extra weight of the centre pixel
-#define RTX_LPT_CW 0
-#endif
+constexpr int kLptRadius = 1;  // 3x3 window (radius 0 was 36 % slower, radius 2 5 % slower)
 __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, uint32_t width, uint32_t rows) {
     const int x = (int)(i % width), y = (int)(i / width);
     uint32_t sum = 0;
-    for (int dy = -RTX_LPT_RADIUS; dy <= RTX_LPT_RADIUS; ++dy) {
+    for (int dy = -kLptRadius; dy <= kLptRadius; ++dy) {
         const int yy = min(max(y + dy, 0), (int)rows - 1);
-        for (int dx = -RTX_LPT_RADIUS; dx <= RTX_LPT_RADIUS; ++dx) {
+        for (int dx = -kLptRadius; dx <= kLptRadius; ++dx) {
             const int xx = min(max(x + dx, 0), (int)width - 1);
             sum += cost[(uint32_t)yy * width + (uint32_t)xx];
         }
     }
-    sum += RTX_LPT_CW * cost[i];
     // scaled to 9 one-sample costs (the 3x3, 1-spp key the tiers were tuned on)
-    constexpr uint32_t kWin = (2 * RTX_LPT_RADIUS + 1) * (2 * RTX_LPT_RADIUS + 1) * kCostSpp;
+    constexpr uint32_t kWin = (2 * kLptRadius + 1) * (2 * kLptRadius + 1) * kCostSpp;
     if (kWin != 9u) sum = (sum * 9u + kWin / 2u) / kWin;
     return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
 }
@@ -1661,11 +1269,11 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
 
 // Heavy-pixel split: with key k ~ a pixel's cost, a lane's share of the
 // frame is W / lanes (W = sum of keys). Pixels whose key exceeds
-// RTX_HEAVY1_ALPHA times it form tier 1 (slots [0, k1): one pixel per wave,
-// 64 lanes per ray). When there are fewer pixels than RTX_HEAVY_RHO per
+// kHeavy1Alpha times it form tier 1 (slots [0, k1): one pixel per wave,
+// 64 lanes per ray). When there are fewer pixels than kHeavyRho per
 // resident lane (a small share of a frame, e.g. one GPU's rows of an 8-GPU
-// split), the tier-1 bar rises to RTX_HEAVY1_ALPHA_SMALL times the share
-// and the pixels above RTX_HEAVY_ALPHA times it (up to that bar) form tier
+// split), the tier-1 bar rises to kHeavy1AlphaSmall times the share
+// and the pixels above kHeavyAlpha times it (up to that bar) form tier
 // 2 (slots [k1, kh), kHeavy2 per wave). Tiers and alphas were chosen with
 // tools/part_scaling.py on C2 split 1/2/4/8 ways. Writes kh to heavy[1] and
 // k1 to heavy[3]. One thread: 256 buckets.
@@ -1674,12 +1282,12 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     double w = 0.0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) w += (double)counts[b] * (double)(kCostBuckets - 1u - b);
     const double share = w / (double)(lanes ? lanes : 1u);
-    const bool small = (double)npix < RTX_HEAVY_RHO * (double)lanes;
-    const double a1 = small ? RTX_HEAVY1_ALPHA_SMALL : RTX_HEAVY1_ALPHA;
-    // a medium share (fewer than RTX_HEAVY_RHO2 pixels per lane, e.g. a
-    // 2- or 4-way split) also gets tier 2 above RTX_HEAVY2_ALPHA_MEDIUM x share
-    const bool medium = !small && (double)npix < RTX_HEAVY_RHO2 * (double)lanes;
-    const double a2 = small ? RTX_HEAVY_ALPHA : medium ? min(RTX_HEAVY2_ALPHA_MEDIUM, a1) : a1;
+    const bool small = (double)npix < kHeavyRho * (double)lanes;
+    const double a1 = small ? kHeavy1AlphaSmall : kHeavy1Alpha;
+    // a medium share (fewer than kHeavyRho2 pixels per lane, e.g. a
+    // 2- or 4-way split) also gets tier 2 above kHeavy2AlphaMedium x share
+    const bool medium = !small && (double)npix < kHeavyRho2 * (double)lanes;
+    const double a2 = small ? kHeavyAlpha : medium ? min(kHeavy2AlphaMedium, a1) : a1;
     uint32_t kh = 0, k1 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
@@ -1728,8 +1336,8 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx = min((RTX_SCAN_PF && S.n_pad > kScanPfMin ? trace_scalar<true>(S, o, d, a, inv_a, t_min, best, list)
-                                                             : trace_scalar<false>(S, o, d, a, inv_a, t_min, best, list)),
+    const int idx = min((S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list)
+                                                             : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list)),
                         (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
@@ -1810,8 +1418,8 @@ static hipError_t allow_lds(const void *kern, size_t lds) {
 }
 
 // k_render with the SGPR double-buffered scan for scenes whose `pre` array
-// does not stay in the scalar cache (RTX_SCAN_PF, kScanPfMin).
-static bool use_pf(const KScene &s) { return RTX_SCAN_PF && s.n_pad > kScanPfMin; }
+// does not stay in the scalar cache (kScanPfMin).
+static bool use_pf(const KScene &s) { return s.n_pad > kScanPfMin; }
 template <bool kPersist, bool kCost>
 static const void *render_fn(bool pf) {
     return pf ? (const void *)k_render<kPersist, kCost, true> : (const void *)k_render<kPersist, kCost, false>;
@@ -1824,12 +1432,18 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
         hipLaunchKernelGGL((k_render<kPersist, kCost, false>), dim3(blocks), dim3(kRB), lds, stream, a);
 }
 
+// Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
+// the block's copy of the spheres for scenes up to kCoopLds.
+static size_t render_lds(const KScene &s) {
+    return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes +
+           (s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
+}
+
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
-    if (RTX_SRC == 0 && p.scene.n_pad > kResidentMax) return hipErrorInvalidValue;
     const bool pf = use_pf(p.scene);
-    const size_t lds = (pf ? list_bytes<true>() : kListBytes) + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
+    const size_t lds = render_lds(p.scene);
     hipError_t e = allow_lds(render_fn<false, true>(pf), lds);
     if (e != hipSuccess) return e;
     launch_k<false, true>(pf, ceil_div(lanes, kRB), lds, stream, p);
@@ -1844,68 +1458,51 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         hipLaunchKernelGGL(k_render_trivial, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, p);
         return hipGetLastError();
     }
-    hipError_t e;
-    if (RTX_SRC == 1 || p.scene.n_pad <= kResidentMax) {
-        const bool pf = use_pf(p.scene);
-        const size_t lds = (pf ? list_bytes<true>() : kListBytes) + kCoopBytes + (RTX_SRC == 1 ? (p.scene.n <= kCoopLds ? (size_t)p.scene.n * (sizeof(float4) + sizeof(float)) : 0) : (size_t)p.scene.n_pad * sizeof(float4));
-        e = allow_lds(render_fn<true, false>(pf), lds);
-        if (e == hipSuccess) e = allow_lds(render_fn<false, false>(pf), lds);
-        if (e == hipSuccess) e = allow_lds(render_fn<true, true>(pf), lds);
-        if (e == hipSuccess) e = allow_lds(render_fn<false, true>(pf), lds);
-        if (e != hipSuccess) return e;
-        if (!RTX_PERSISTENT || !sched.cost || p.spp < kLptMinSpp) {
-            launch_k<false, false>(pf, need, lds, stream, p);
-            return hipGetLastError();
-        }
-        if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
-        // 1. cost pre-pass: kCostSpp samples per pixel, segments only
-        KParams c = p;
-        c.spp = min(p.spp, kCostSpp);
-        c.cost_out = sched.cost;
-        c.state = RTX_LPT_RESUME ? sched.state : nullptr;  // the first kCostSpp samples, not traced again
-        if (!RTX_LPT_RESUME) c.counters = p.counters + 3;     // scratch: not part of the frame's count
-        c.accum = nullptr;
-        c.wave_times = nullptr;
-        c.perm = nullptr;  // index order
-        c.heavy = nullptr;
-        c.prio_slots = 0;
-        e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
-        if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-#if RTX_LPT_PERSIST_PREPASS
-        // persistent lanes: a lane whose pixel ends takes the next one, so the
-        // pass does not wait on each wave's slowest pixel
-        const uint32_t cblocks = min(need, resident_blocks(render_fn<true, true>(pf), lds));
-        launch_k<true, true>(pf, cblocks, lds, stream, c);
-#else
-        launch_k<false, true>(pf, need, lds, stream, c);
-#endif
-        // 2. counting sort by cost, descending
-        const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
-        hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                           p.rows_local, sched.buckets);
-        // 3. heavy-pixel split (from the histogram), the ordered queue, then
-        // the persistent render over it
-        const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
-        uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
-        hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
-        hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                           p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
-        KParams q = p;
-        q.perm = sched.perm;
-        q.state = RTX_LPT_RESUME ? sched.state : nullptr;
-        q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * RTX_PRIO_FRAC_X100 / 100u);
-        q.heavy = RTX_HEAVY_WAVE ? heavy : nullptr;
-        e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        launch_k<true, false>(pf, blocks, lds, stream, q);
-    } else {
-        const size_t lds = kListBytes + kChunk * sizeof(float4);
-        e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        const uint32_t blocks = min(need, resident_blocks((const void *)k_render_streamed, lds));
-        hipLaunchKernelGGL(k_render_streamed, dim3(blocks), dim3(kRB), lds, stream, p);
+    const bool pf = use_pf(p.scene);
+    const size_t lds = render_lds(p.scene);
+    hipError_t e = allow_lds(render_fn<true, false>(pf), lds);
+    if (e == hipSuccess) e = allow_lds(render_fn<false, false>(pf), lds);
+    if (e == hipSuccess) e = allow_lds(render_fn<false, true>(pf), lds);
+    if (e != hipSuccess) return e;
+    if (!sched.cost || p.spp < kLptMinSpp) {
+        launch_k<false, false>(pf, need, lds, stream, p);
+        return hipGetLastError();
     }
+    if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
+    // 1. cost pre-pass: kCostSpp samples per pixel; records each pixel's
+    // segments and its state (acc, seed) after them, which the render resumes
+    KParams c = p;
+    c.spp = min(p.spp, kCostSpp);
+    c.cost_out = sched.cost;
+    c.state = sched.state;
+    c.accum = nullptr;
+    c.wave_times = nullptr;
+    c.perm = nullptr;  // index order
+    c.heavy = nullptr;
+    c.prio_slots = 0;
+    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    launch_k<false, true>(pf, need, lds, stream, c);
+    // 2. counting sort by cost, descending
+    const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
+    hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
+                       p.rows_local, sched.buckets);
+    // 3. heavy-pixel split (from the histogram), the ordered queue, then
+    // the persistent render over it
+    const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
+    uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
+    hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
+    hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
+                       p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
+    KParams q = p;
+    q.perm = sched.perm;
+    q.state = sched.state;
+    q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * kPrioFracX100 / 100u);
+    q.heavy = heavy;
+    e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    launch_k<true, false>(pf, blocks, lds, stream, q);
     return hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_create": (C.c_int, [C.c_int, C.POINTER(ctx)]),
         "rtx_destroy": (None, [ctx]),
         "rtx_set_stream": (C.c_int, [ctx, vp]),
+        "rtx_use_own_stream": (C.c_int, [ctx]),
         "rtx_upload_world": (C.c_int, [ctx, C.POINTER(rtx_world)]),
         "rtx_set_frame": (C.c_int, [ctx, C.POINTER(rtx_frame)]),
         "rtx_render_rows": (C.c_int, [ctx, u32, u32, u32, vp]),
@@ -272,7 +273,12 @@ class Context:
             pass
 
     def set_stream(self, stream: Optional[int]):
-        _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream or 0)), "rtx_set_stream")
+        """Launch on `stream` (a hipStream_t handle; 0 = HIP's null stream,
+        i.e. torch's default stream); None = the context's own stream."""
+        if stream is None:
+            _check(self._lib.rtx_use_own_stream(self._h), "rtx_use_own_stream")
+        else:
+            _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream)), "rtx_set_stream")
 
     def upload_world(self, world: World):
         w = world.as_struct()

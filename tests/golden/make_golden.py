@@ -15,6 +15,12 @@ Fixtures (all doubles exact; t_max null = +inf):
   camera_simple_400x225.json  Camera(400,225).get_ray(u,v)      (Camera.h:23-26)
   hit_test_world.json         Hittable_list::hit over test_world (Hittable_list.cpp:3-20)
   hit_rtiow9.json             Hittable_list::hit over random_world(9), 326 spheres
+  hit_rtiow11.npz             ... over random_world(11), 486 spheres (the bench scene, C2/C3):
+                              camera rays + secondary rays + grazing rays (tests/cases.py)
+  hit_c5_100k.npz             ... over random_world(159) truncated to 100,000 spheres (C5): camera
+                              and secondary rays; the scene is named by generator + sha256 digest
+                              (tests/cases.py scene_digest), not stored
+npz fixtures hold float64 arrays only (np.load(..., allow_pickle=False)).
 """
 import json
 import os
@@ -25,7 +31,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle as orc  # noqa: E402
+from cases import camera_rays, grazing_rays, scene_digest  # noqa: E402
 
 
 def fmt(x: float) -> str:
@@ -104,6 +112,30 @@ def main():
                "spheres": sph9.tolist(), "rays": rays9.tolist(),
                "cases": [{"t_min": 0.001, "t_max": None, "expected": hits}]},
               open(os.path.join(HERE, "hit_rtiow9.json"), "w"))
+
+    # 4. random_world(11) (486 spheres): primary + secondary + grazing rays.
+    sph11, _, _ = orc.random_world(11)
+    rng11 = np.random.default_rng(486)
+    fr = orc.camera_look_at(1920, 1080)
+    prim = camera_rays(fr, 300, rng11)
+    sec = random_rays(rng11, 300, [-13, 0.0, -13], [13, 1.5, 13], True)
+    graz = grazing_rays(sph11, 2000, rng11, ext_frac=0.0).astype(np.float64)
+    sph11 = f32(sph11)
+    for name, rays in (("hit_rtiow11.npz", np.concatenate([prim, sec])), ("hit_grazing11.npz", graz)):
+        hits, _ = run_ref(sph11.tolist(), rays.tolist(), 0.001, None)
+        np.savez_compressed(os.path.join(HERE, name), spheres=sph11, rays=rays,
+                            expected=np.array(hits, np.float64), t_min=np.float64(0.001))
+
+    # 5. the C5 scene: random_world(159) truncated to 100,000 spheres.
+    sph5, _, _ = orc.random_world(159, 100000)
+    rng5 = np.random.default_rng(100000)
+    prim5 = camera_rays(fr, 200, rng5)
+    sec5 = random_rays(rng5, 200, [-30, 0.0, -30], [30, 1.5, 30], True)
+    rays5 = np.concatenate([prim5, sec5])
+    hits, _ = run_ref(f32(sph5).tolist(), rays5.tolist(), 0.001, None)
+    np.savez_compressed(os.path.join(HERE, "hit_c5_100k.npz"), rays=rays5, expected=np.array(hits, np.float64),
+                        t_min=np.float64(0.001), grid=np.float64(159), count=np.float64(len(sph5)),
+                        digest=np.frombuffer(bytes.fromhex(scene_digest(sph5)), np.uint8))
     print("golden vectors written to", HERE)
 
 

