@@ -81,6 +81,9 @@ struct rtx_ctx {
     // LPT scheduling scratch (persistent kernel): cost + perm per pixel
     uint32_t *d_sched = nullptr;
     size_t sched_pixels = 0;
+    // per-sample RNG kernel's per-wave sample-colour scratch
+    float *d_ps = nullptr;
+    size_t ps_floats = 0;
     EventPair events[kEventRing];   // ring: [ev_head, ev_head + ev_count) outstanding
     size_t ev_head = 0, ev_count = 0;
     double ms_folded = 0.0;         // durations of launches whose pair was recycled
@@ -191,6 +194,7 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipFree(c->d_counters);
     (void)hipFree(c->d_wave_times);
     (void)hipFree(c->d_sched);
+    (void)hipFree(c->d_ps);
     for (auto &p : c->events) {
         if (p.start) (void)hipEventDestroy(p.start);
         if (p.stop) (void)hipEventDestroy(p.stop);
@@ -451,7 +455,18 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix) * sizeof(uint32_t)));
         c->sched_pixels = npix;
     }
+    const size_t ps_need = rtx::ps_scratch_floats(p);
+    if (ps_need > c->ps_floats) {
+        RTX_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_ps);
+        c->d_ps = nullptr;
+        c->ps_floats = 0;
+        RTX_HIP(hipMalloc(&c->d_ps, ps_need * sizeof(float)));
+        c->ps_floats = ps_need;
+    }
     rtx::KSchedule sched;
+    sched.ps_scratch = c->d_ps;
+    sched.ps_floats = c->ps_floats;
     sched.cost = c->d_sched;
     sched.perm = c->d_sched + c->sched_pixels;
     sched.buckets = c->d_sched + 2 * c->sched_pixels;

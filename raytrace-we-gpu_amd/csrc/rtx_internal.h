@@ -61,6 +61,10 @@ struct KParams {
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
+    // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
+    // [wave][2 slots][3 channels][ps_cap], ps_px pixels per batch
+    float *ps_scratch;
+    uint32_t ps_px, ps_cap;
 };
 
 // Longest-processing-time-first scheduling for the persistent kernel: a
@@ -75,6 +79,8 @@ struct KSchedule {
     uint32_t *buckets;  // [2 * nbuckets + 4]: counts, cursors, heavy counters and ends (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
+    float *ps_scratch;  // k_render_ps scratch (rng_mode 1), ps_floats floats
+    size_t ps_floats;
 };
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
@@ -82,6 +88,9 @@ constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than i
 constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)
 
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream);
+// Floats of k_render_ps scratch a launch with these parameters needs (0 when
+// it takes another kernel).
+size_t ps_scratch_floats(const KParams &p);
 hipError_t launch_cost(const KParams &p, hipStream_t stream);  // exact grid, p.cost_out set
 hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,
                                uint32_t height, uint32_t tile_rows, uint32_t nparts,

@@ -23,6 +23,8 @@
 //    accepted one.
 // Measured-and-rejected variants (LDS-resident spheres, pre-prefilter scans,
 // ...) are in git history and DESIGN.md §7.
+#include <algorithm>
+
 #include "rtx_device_math.h"
 #include "rtx_internal.h"
 #include "rtx_prefilter.h"
@@ -785,26 +787,16 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
     L.bounce = 0;
 }
 
-// Shading of one finished hit_world call (sample_color body, :262-284, and
-// scatter, :207-252). Advances the lane to its next sample when the path
-// ends; clears `active` after the pixel's last sample.
-template <bool kCost = false>
-__device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
-    if constexpr (kCost) {  // scheduling pre-pass: record the pixel's segments
-        P.cost_out[L.gid] = L.segs - L.seg0;
-        // and its state after these samples: the render resumes from it
-        if (P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
-        return;
-    }
-    // accColor /= spp; toGamma; float4(c, 1)  (:312-314)
-    f3 sum = L.acc;
+// accColor /= spp; toGamma; float4(c, 1) (:312-314) for local pixel gid,
+// whose linear sample sum is `sum`.
+__device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 sum) {
     float n = (float)P.spp;
     if (P.accum) {  // progressive: running linear sum over frames
-        float4 a = P.accum[L.gid];
+        float4 a = P.accum[gid];
         a.x = a.x + sum.x;
         a.y = a.y + sum.y;
         a.z = a.z + sum.z;
-        P.accum[L.gid] = a;
+        P.accum[gid] = a;
         sum = mk3(a.x, a.y, a.z);
         n = (float)(P.accum_frames * P.spp);
     }
@@ -813,7 +805,19 @@ __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
     o.y = to_gamma(sum.y / n);
     o.z = to_gamma(sum.z / n);
     o.w = 1.0f;
-    P.out[L.gid] = o;
+    P.out[gid] = o;
+}
+
+// A pixel's output (output_pixel), or the scheduling pre-pass's record of it.
+template <bool kCost = false>
+__device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
+    if constexpr (kCost) {  // scheduling pre-pass: record the pixel's segments
+        P.cost_out[L.gid] = L.segs - L.seg0;
+        // and its state after these samples: the render resumes from it
+        if (P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
+        return;
+    }
+    output_pixel(P, L.gid, L.acc);
 }
 
 // Diffuse direction before normalisation, target - p (ShaderCompute.hlsl:
@@ -826,10 +830,15 @@ __device__ __forceinline__ f3 lambert_guard(f3 v, f3 nrm, bool guard) {
     return guard && nz ? nrm : v;
 }
 
-template <bool kCost = false>
-__device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
-    L.segs++;
-    bool ended = false;
+// One finished hit_world call of sample_color (:262-284). On a hit, scatter
+// (:207-252) moves the lane's ray (o, d, a, inv_a) and multiplies col by the
+// attenuation; the path goes on unless the material does not scatter or the
+// depth is exhausted (black, :286). On a miss, `sky_col` = col * the sky
+// gradient (:279-283), the sample's colour. LaneT: any lane state with o, d,
+// a, inv_a, col, seed, bounce (Lane, PsLane).
+enum { kSegContinue = 0, kSegSky = 1, kSegBlack = 2 };
+template <typename LaneT>
+__device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit, float t, f3 &sky_col) {
     if (hit >= 0) {
         const KScene &S = P.scene;
         const float4 sc = S.cen[hit];
@@ -841,7 +850,6 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
         const int mt = S.mtype[hit];
         const float4 mv = S.mval[hit];
         f3 dir;
-        bool scattered = true;
         // Lambert and metal share random_in_unit_sphere and normalize: run
         // them once for both kinds of lane (each lane's ops are the HLSL's).
         if (mt == 0 || mt == 1) {
@@ -862,24 +870,33 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
             const float h = hash1(L.seed);
             dir = (cant || refl > h) ? reflect3(ud, nrm) : refract3(ud, nrm, ratio);
         } else {
-            scattered = false;  // unknown material: sample is black (:251, :274)
+            return kSegBlack;  // unknown material: sample is black (:251, :274)
         }
-        if (scattered) {
-            L.o = p;
-            set_dir(L, dir);
-            L.bounce++;
-            ended = L.bounce >= P.depth;  // depth exhausted -> black (:286)
-        } else {
-            ended = true;
-        }
-    } else {  // miss: sky gradient (:279-283)
-        const f3 ud = normalize3(L.d);
-        const float tt = 0.5f * (ud.y + 1.0f);
-        const float w = 1.0f - tt;
-        const f3 sky = mk3(w + tt * 0.5f, w + tt * 0.7f, w + tt);
-        L.acc = L.acc + L.col * sky;
-        ended = true;
+        L.o = p;
+        L.d = dir;
+        L.a = dir_len2(dir);
+        L.inv_a = 1.0f / L.a;
+        L.bounce++;
+        return L.bounce >= P.depth ? kSegBlack : kSegContinue;  // depth exhausted -> black (:286)
     }
+    const f3 ud = normalize3(L.d);
+    const float tt = 0.5f * (ud.y + 1.0f);
+    const float w = 1.0f - tt;
+    const f3 sky = mk3(w + tt * 0.5f, w + tt * 0.7f, w + tt);
+    sky_col = L.col * sky;
+    return kSegSky;
+}
+
+// Chain-RNG lane: one segment, then the pixel's next sample when the path
+// ends (acc += colour in sample order, :269-284), or the pixel's output
+// after its last sample (clears `active`).
+template <bool kCost = false>
+__device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
+    L.segs++;
+    f3 c;
+    const int r = path_segment(P, L, hit, t, c);
+    if (r == kSegSky) L.acc = L.acc + c;
+    const bool ended = r != kSegContinue;
     if (ended) {
         L.sample++;
         if (L.sample >= P.spp) {
@@ -1298,6 +1315,179 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     heavy[3] = k1;
 }
 
+// ---- per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample) --
+// Every (pixel, sample) has its own seed (pixel_seed), so samples are
+// independent and the north star's kernel shape applies: a lane traces ONE
+// sample. A wave takes batches of ps_px consecutive pixels from the global
+// queue (one atomic per batch); the batch's ps_px * spp items (pixel-major:
+// item = po * spp + s) go to the wave's lanes as they free up, so lanes stay
+// busy across path lengths (1..depth segments) without waiting for each
+// other. A finished sample stores its colour (col * sky, or +0 for a black
+// path) into the wave's scratch at [channel][s * npx + po]; when all items of
+// a batch are done, lane po folds its pixel's colours IN SAMPLE ORDER —
+// acc = ((0 + c_0) + c_1) + ... — which is bit for bit the reference's
+// accumulation (:304-312; adding +0 for a black sample leaves acc unchanged:
+// acc starts at +0 and is never -0), and the batch's pixels are written with
+// one coalesced store. Two batch slots per wave: lanes start on the next
+// batch while the previous one's last samples finish.
+struct PsLane {
+    f3 o, d, col;
+    float a, inv_a, seed;
+    uint32_t bounce, segs;
+    uint32_t slot;  // physical batch slot (0/1) of the sample
+    uint32_t sidx;  // s * npx + po: the sample's scratch index
+    bool active;
+};
+struct PsSlot {  // wave-uniform
+    uint32_t phys, px0, npx, total, issued, done;
+    bool live;
+};
+
+__device__ __forceinline__ void ps_start(const KParams &P, const Frame &F, const PsSlot &B, uint32_t item,
+                                         PsLane &L) {
+    const uint32_t po = item / P.spp;
+    const uint32_t s = item - po * P.spp;
+    uint32_t x, y;
+    lane_pixel(P, B.px0 + po, x, y);
+    L.seed = pixel_seed(P, x, y, s);
+    f3 o, d;
+    start_sample(F, x, y, L.seed, o, d);
+    L.o = o;
+    L.d = d;
+    L.a = dir_len2(d);
+    L.inv_a = 1.0f / L.a;
+    L.col = mk3(1.0f, 1.0f, 1.0f);
+    L.bounce = 0;
+    L.slot = B.phys;
+    L.sidx = s * B.npx + po;
+    L.active = true;
+}
+
+// Fold a completed batch (all lanes of the wave call it; lane po < npx owns
+// pixel px0 + po) and write its pixels.
+__device__ __forceinline__ void ps_fold(const KParams &P, const PsSlot &B, const float *scr) {
+    __threadfence();  // this wave's scratch stores are done; its loads below miss the stale L1
+    const uint32_t po = threadIdx.x & 63u;
+    if (po >= B.npx) return;
+    const float *c0 = scr + (size_t)B.phys * 3 * P.ps_cap;
+    const float *c1 = c0 + P.ps_cap;
+    const float *c2 = c1 + P.ps_cap;
+    f3 acc = mk3(0.0f, 0.0f, 0.0f);
+    const uint32_t n = B.npx;
+    uint32_t s = 0;
+    for (; s + 4 <= P.spp; s += 4) {  // four samples' loads in flight, adds in order
+        float x[4], y[4], z[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = (s + k) * n + po;
+            x[k] = c0[i];
+            y[k] = c1[i];
+            z[k] = c2[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = acc + mk3(x[k], y[k], z[k]);
+    }
+    for (; s < P.spp; ++s) {
+        const uint32_t i = s * n + po;
+        acc = acc + mk3(c0[i], c1[i], c2[i]);
+    }
+    output_pixel(P, B.px0 + po, acc);
+}
+
+template <bool kPF>
+__global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
+    // dynamic LDS: [candidate list, list_bytes<kPF>][LDS copy of the spheres (n <= kCoopLds)]
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
+    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
+    constexpr uint32_t kLB = list_bytes<kPF>();
+    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB);
+    float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
+    const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
+    if (sph_lds) {
+        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
+            s_pre4[i] = P.scene.pre4[i];
+            s_rad[i] = P.scene.cen[i].w;
+        }
+        __syncthreads();
+    }
+    const int last = (int)P.scene.n - 1;
+    const Frame F = load_frame(P);
+    const uint32_t npix = P.rows_local * P.width;
+    const uint32_t wave = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
+    float *scr = P.ps_scratch + (size_t)wave * 6 * P.ps_cap;  // [phys slot][channel][ps_cap]
+    const uint32_t lane = threadIdx.x & 63u;
+    PsLane L;
+    L.active = false;
+    L.segs = 0;
+    PsSlot A{0, 0, 0, 0, 0, 0, false}, B{1, 0, 0, 0, 0, 0, false};  // A: the slot being issued
+    bool exhausted = false;
+    for (;;) {
+        // hand the idle lanes the next items: of batch A, then of a new batch
+        for (int pass = 0; pass < 2; ++pass) {
+            const uint64_t idle = __ballot(!L.active);
+            if (idle == 0ull) break;
+            if (!A.live || A.issued == A.total) {
+                if (exhausted || B.live) break;
+                uint32_t base = 0;
+                if (lane == 0u) base = atomicAdd(P.queue, P.ps_px);
+                base = (uint32_t)__shfl((int)base, 0, 64);
+                if (base >= npix) {
+                    exhausted = true;
+                    break;
+                }
+                B.live = true;
+                B.px0 = base;
+                B.npx = min(P.ps_px, npix - base);
+                B.total = B.npx * P.spp;
+                B.issued = 0;
+                B.done = 0;
+                const PsSlot t = A;
+                A = B;
+                B = t;
+            }
+            const uint32_t take = min((uint32_t)__popcll(idle), A.total - A.issued);
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (!L.active && rank < take) ps_start(P, F, A, A.issued + rank, L);
+            A.issued += take;
+        }
+        if (__ballot(L.active) == 0ull) break;  // queue exhausted and every batch folded
+        bool ended = false;
+        if (L.active) {
+            float best = __uint_as_float(0x7f800000u);
+            const int hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene,
+                                                            [s_pre4, s_rad](uint32_t i) {
+                                                                const float4 c = s_pre4[i];
+                                                                return make_float4(c.x, c.y, c.z, s_rad[i]);
+                                                            },
+                                                            L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                                    : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+            L.segs++;
+            f3 c = mk3(0.0f, 0.0f, 0.0f);
+            const int r = path_segment(P, L, min(hit, last), best, c);
+            if (r != kSegContinue) {
+                float *o = scr + (size_t)L.slot * 3 * P.ps_cap + L.sidx;
+                o[0] = c.x;  // +0 for a black path
+                o[P.ps_cap] = c.y;
+                o[2 * P.ps_cap] = c.z;
+                L.active = false;
+                ended = true;
+            }
+        }
+        A.done += (uint32_t)__popcll(__ballot(ended && L.slot == A.phys));
+        B.done += (uint32_t)__popcll(__ballot(ended && L.slot == B.phys));
+        if (A.live && A.done == A.total) {
+            ps_fold(P, A, scr);
+            A.live = false;
+        }
+        if (B.live && B.done == B.total) {
+            ps_fold(P, B, scr);
+            B.live = false;
+        }
+    }
+    count_segments(P, L.segs);
+}
+
 // spp == 0 or depth == 0: no segment is traced; the pixel is
 // toGamma(0 / spp) (accColor stays 0; 0/0 = NaN for spp == 0, :312-313).
 __global__ void __launch_bounds__(kBlock) k_render_trivial(const KParams P) {
@@ -1450,6 +1640,50 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// Per-sample launches: items per batch slot. A batch is ps_px pixels with
+// ps_px * spp <= ps_cap items; about 8 batches per resident wave keep the
+// waves balanced at the end of a frame share.
+constexpr uint32_t kPsItems = 4096;
+static size_t ps_lds(const KScene &s) {
+    return (use_pf(s) ? list_bytes<true>() : kListBytes) +
+           (!use_pf(s) && s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
+}
+static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }
+static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
+static uint32_t ps_waves(const KParams &p) {
+    const bool pf = use_pf(p.scene);
+    const uint32_t npix = p.rows_local * p.width;
+    const uint32_t blocks = min(ceil_div(npix, kRB), resident_blocks(ps_fn(pf), ps_lds(p.scene)));
+    return blocks * (kRB / 64);
+}
+size_t ps_scratch_floats(const KParams &p) {
+    if (p.rng_mode != 1u || p.spp == 0 || p.depth == 0 || (uint64_t)p.rows_local * p.width == 0) return 0;
+    return (size_t)ps_waves(p) * 6 * ps_cap_of(p.spp);
+}
+static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_t stream) {
+    const bool pf = use_pf(p.scene);
+    const size_t lds = ps_lds(p.scene);
+    hipError_t e = allow_lds(ps_fn(pf), lds);
+    if (e != hipSuccess) return e;
+    const uint32_t npix = p.rows_local * p.width;
+    const uint32_t waves = ps_waves(p);
+    KParams q = p;
+    q.ps_cap = ps_cap_of(p.spp);
+    q.ps_scratch = sched.ps_scratch;
+    if (!q.ps_scratch || sched.ps_floats < (size_t)waves * 6 * q.ps_cap) return hipErrorInvalidValue;
+    const uint64_t items = (uint64_t)npix * p.spp;
+    const uint64_t target = std::min<uint64_t>(std::max<uint64_t>(items / ((uint64_t)waves * 8u), 64u), kPsItems);
+    q.ps_px = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(64u, target / p.spp));
+    e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = waves / (kRB / 64);
+    if (pf)
+        hipLaunchKernelGGL(k_render_ps<true>, dim3(blocks), dim3(kRB), lds, stream, q);
+    else
+        hipLaunchKernelGGL(k_render_ps<false>, dim3(blocks), dim3(kRB), lds, stream, q);
+    return hipGetLastError();
+}
+
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
@@ -1458,6 +1692,7 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
         hipLaunchKernelGGL(k_render_trivial, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, p);
         return hipGetLastError();
     }
+    if (p.rng_mode == 1u) return launch_ps(p, sched, stream);  // one lane per (pixel, sample)
     const bool pf = use_pf(p.scene);
     const size_t lds = render_lds(p.scene);
     hipError_t e = allow_lds(render_fn<true, false>(pf), lds);

@@ -332,6 +332,93 @@ def test_lpt_schedule_and_pixel_cost(gpu_ctx, oracle, rtx):
 
 
 # ---------------------------------------------------------------------------
+# per-sample RNG: one lane per (pixel, sample) (k_render_ps)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("ext,w,h,spp,depth", [
+    (11, 96, 54, 100, 50),   # batches of 40 pixels
+    (11, 64, 36, 1, 50),     # one sample per pixel: 64-pixel batches, lanes wait for folds
+    (11, 33, 17, 7, 3),      # ragged last batch, shallow paths
+    (4, 3, 2, 5000, 20),     # spp > 4096: one pixel per batch, scratch sized by spp
+    (20, 48, 27, 9, 50),     # > kScanPfMin spheres: the kPF scan
+])
+def test_per_sample_kernel_bit_exact(gpu_ctx, oracle, rtx, ext, w, h, spp, depth):
+    """rng_mode 1 takes k_render_ps: lanes trace single samples of a batch
+    of pixels, each pixel's sample colours are folded in sample order; the
+    frame and its segment count equal the oracle's (pixel by pixel, samples
+    in order, one seed per (pixel, sample))."""
+    world = rtx.random_world(ext, depth=depth, spp=spp)
+    frame = rtx.camera_look_at(w, h, aspect=w / h)
+    frame.rng_mode = 1
+    img, st = render_gpu(gpu_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(h), nthreads=8)
+    assert_bits_equal(img, want, f"per-sample {w}x{h} spp {spp}")
+    assert st.segments == segs
+    assert st.samples == w * h * spp
+
+
+def test_per_sample_options_and_parts(gpu_ctx, oracle, rtx):
+    """k_render_ps with thin lens, frame_index, the Lambert guard, a 5-way
+    row split and progressive accumulation: bit-exact in every case."""
+    W, H, spp = 80, 45, 12
+    world = rtx.random_world(11, depth=50, spp=spp)
+
+    def fr():
+        f = rtx.camera_look_at(W, H, aspect=W / H)
+        f.rng_mode = 1
+        return f
+    lens = rtx.set_aperture(fr(), 0.4)
+    idx = fr()
+    idx.frame_index = 5
+    guard = fr()
+    guard.flags = rtx.FRAME_LAMBERT_GUARD
+    for name, f in (("thin lens", lens), ("frame_index", idx), ("lambert guard", guard)):
+        img, st = render_gpu(gpu_ctx, world, f)
+        want, segs = oracle.render_rows(world, f, np.arange(H), nthreads=8)
+        assert_bits_equal(img, want, f"per-sample {name}")
+        assert st.segments == segs
+    f = fr()
+    gpu_ctx.set_frame(f)
+    buf = gpu_ctx.alloc((H, W, 4))
+    for part in range(5):
+        rows = rtx.part_row_ids(H, 4, part, 5)
+        gpu_ctx.render_rows(4, part, 5, buf.ptr)
+        got = buf.numpy().reshape(-1)[: len(rows) * W * 4].reshape(len(rows), W, 4)
+        want, _ = oracle.render_rows(world, f, rows, nthreads=8)
+        assert_bits_equal(got, want, f"per-sample part {part} of 5")
+    buf.free()
+    total = np.zeros((H, W, 3), np.float32)
+    for k in range(2):
+        gpu_ctx.accumulate(reset=(k == 0))
+        g = fr()
+        g.frame_index = k
+        lin, _ = oracle.render_rows_linear(world, g, np.arange(H), nthreads=8)
+        total = total + lin[..., :3]
+    mean = (total / np.float32(2 * spp)).astype(np.float32)
+    want = oracle.math("pow", mean.ravel(), np.full(mean.size, 0.454545454545, np.float32)).reshape(mean.shape)
+    assert_bits_equal(gpu_ctx.download()[..., :3], want, "per-sample accumulation")
+
+
+def test_per_sample_c2_rows(gpu_ctx, oracle, rtx):
+    """The C2 frame (1920x1080, 486 spheres, spp 100, depth 50) in per-sample
+    mode: 24 rows bit-exact against the oracle, and one rank's share of an
+    8-way split bit-exact too."""
+    world = rtx.random_world(11, depth=50, spp=100)
+    frame = rtx.camera_look_at(1920, 1080)
+    frame.rng_mode = 1
+    img, st = render_gpu(gpu_ctx, world, frame)
+    assert st.samples == 1920 * 1080 * 100
+    rows = np.arange(13, 1080, 45)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img[rows], want, "per-sample C2 rows")
+    ids = rtx.part_row_ids(1080, 5, 6, 8)
+    buf = gpu_ctx.alloc((len(ids), 1920, 4))
+    gpu_ctx.render_rows(5, 6, 8, buf.ptr)
+    got = buf.numpy()
+    buf.free()
+    assert_bits_equal(got, img[ids], "per-sample part 6 of 8 vs the whole frame")
+
+
+# ---------------------------------------------------------------------------
 # row-tile partitions (the multi-GPU data path) on one device
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("nparts,tile_rows", [(2, 8), (3, 5), (8, 5), (8, 1), (5, 64)])
@@ -481,6 +568,17 @@ def test_overflow_and_fallback_paths_bit_exact(stress_ctx, oracle, rtx, nparts, 
     buf.free()
     want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
     assert_bits_equal(got, want, f"stress build, part {part} of {nparts}")
+
+
+def test_per_sample_stress_build(stress_ctx, oracle, rtx):
+    """k_render_ps with every candidate list overflowing (stress build)."""
+    world = rtx.random_world(11, depth=50, spp=6)
+    frame = rtx.camera_look_at(64, 36, aspect=64 / 36)
+    frame.rng_mode = 1
+    img, st = render_gpu(stress_ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(36), nthreads=8)
+    assert_bits_equal(img, want, "per-sample, stress build")
+    assert st.segments == segs
 
 
 @pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])

@@ -21,12 +21,14 @@ ap.add_argument("--parts", type=int, nargs="*", default=[1, 2, 4, 8])
 ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--tile-rows", type=int, default=5)
 ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
 ap.add_argument("libs", nargs="*")
 a = ap.parse_args()
 
 W, H = 1920, 1080
 world = rtx.random_world(11, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
+frame.rng_mode = 1 if a.rng == "per-sample" else 0
 for path in a.libs or [None]:
     lib = rtx.load_library(path) if path else None
     ctx = rtx.Context(0, lib=lib)
@@ -47,7 +49,7 @@ for path in a.libs or [None]:
         crit = max(times)
         if R == 1:
             t1 = crit
-        rep = {"lib": os.path.basename(path) if path else "default", "parts": R,
+        rep = {"lib": os.path.basename(path) if path else "default", "rng": a.rng, "parts": R,
                "part_ms": [round(t, 3) for t in times], "critical_ms": round(crit, 3),
                "mean_ms": round(sum(times) / R, 3)}
         if t1:
