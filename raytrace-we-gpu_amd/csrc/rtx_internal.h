@@ -62,7 +62,7 @@ struct KParams {
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
-    // [wave][2 slots][3 channels][ps_cap], ps_px pixels per batch
+    // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
     float *ps_scratch;
     uint32_t ps_px, ps_cap;
 };

@@ -24,6 +24,8 @@
 // Measured-and-rejected variants (LDS-resident spheres, pre-prefilter scans,
 // ...) are in git history and DESIGN.md §7.
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "rtx_device_math.h"
 #include "rtx_internal.h"
@@ -77,6 +79,9 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 #endif
 #ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
 #define RTX_DIAG_PIXEL 0
+#endif
+#ifndef RTX_PS_DIAG_NOSTORE  // timing diagnostic: k_render_ps drops its sample colours (WRONG images)
+#define RTX_PS_DIAG_NOSTORE 0
 #endif
 #ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
 #define RTX_DIAG_COOP 0
@@ -1318,37 +1323,44 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
 // ---- per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample) --
 // Every (pixel, sample) has its own seed (pixel_seed), so samples are
 // independent and the north star's kernel shape applies: a lane traces ONE
-// sample. A wave takes batches of ps_px consecutive pixels from the global
-// queue (one atomic per batch); the batch's ps_px * spp items (pixel-major:
-// item = po * spp + s) go to the wave's lanes as they free up, so lanes stay
-// busy across path lengths (1..depth segments) without waiting for each
-// other. A finished sample stores its colour (col * sky, or +0 for a black
-// path) into the wave's scratch at [channel][s * npx + po]; when all items of
-// a batch are done, lane po folds its pixel's colours IN SAMPLE ORDER —
+// sample. A wave takes batches of consecutive pixels from the global queue
+// (one atomic per batch); a batch's npx * spp items (pixel-major: item =
+// po * spp + s) go to the wave's lanes as they free up, so lanes stay busy
+// across path lengths (1..depth segments) without waiting for each other. A
+// finished sample stores its colour (col * sky, or +0 for a black path) into
+// the wave's scratch at [slot][s * npx + po] (float4); when all items of a
+// batch are done, lane po folds its pixel's colours IN SAMPLE ORDER —
 // acc = ((0 + c_0) + c_1) + ... — which is bit for bit the reference's
 // accumulation (:304-312; adding +0 for a black sample leaves acc unchanged:
 // acc starts at +0 and is never -0), and the batch's pixels are written with
-// one coalesced store. Two batch slots per wave: lanes start on the next
-// batch while the previous one's last samples finish.
+// one coalesced store.
+// kPsSlots batch slots per wave: lanes move on to new batches while earlier
+// ones wait for a long path; a wave stalls only when every slot holds an
+// unfinished, fully issued batch. Batches are ps_px pixels (<= ps_cap
+// items; the host makes them smaller for a small frame share, so that every
+// wave gets ~20 and the waves finish together). Scratch stays small
+// (kPsSlots * ps_cap * 16 B per wave: in the 256 MB MALL), which measured
+// faster than large batches (A/B in DESIGN.md §7). Once the queue is empty
+// and a wave has at most kCoopMax samples left, it traces them with the
+// group coop of the chain kernel (several lanes per ray), at a raised wave
+// priority: the frame's last, longest paths end sooner.
+constexpr int kPsSlots = 4;
+constexpr uint32_t kPsStateBytes = (kRB / 64) * kPsSlots * 4 * sizeof(uint32_t);  // per block
 struct PsLane {
     f3 o, d, col;
     float a, inv_a, seed;
     uint32_t bounce, segs;
-    uint32_t slot;  // physical batch slot (0/1) of the sample
-    uint32_t sidx;  // s * npx + po: the sample's scratch index
+    uint32_t slot;  // batch slot of the sample
+    uint32_t sidx;  // s * npx + po: the sample's scratch index in its slot
     bool active;
 };
-struct PsSlot {  // wave-uniform
-    uint32_t phys, px0, npx, total, issued, done;
-    bool live;
-};
 
-__device__ __forceinline__ void ps_start(const KParams &P, const Frame &F, const PsSlot &B, uint32_t item,
-                                         PsLane &L) {
+__device__ __forceinline__ void ps_start(const KParams &P, const Frame &F, uint32_t px0, uint32_t npx,
+                                         uint32_t slot, uint32_t item, PsLane &L) {
     const uint32_t po = item / P.spp;
     const uint32_t s = item - po * P.spp;
     uint32_t x, y;
-    lane_pixel(P, B.px0 + po, x, y);
+    lane_pixel(P, px0 + po, x, y);
     L.seed = pixel_seed(P, x, y, s);
     f3 o, d;
     start_sample(F, x, y, L.seed, o, d);
@@ -1358,76 +1370,81 @@ __device__ __forceinline__ void ps_start(const KParams &P, const Frame &F, const
     L.inv_a = 1.0f / L.a;
     L.col = mk3(1.0f, 1.0f, 1.0f);
     L.bounce = 0;
-    L.slot = B.phys;
-    L.sidx = s * B.npx + po;
+    L.slot = slot;
+    L.sidx = s * npx + po;
     L.active = true;
 }
 
-// Fold a completed batch (all lanes of the wave call it; lane po < npx owns
-// pixel px0 + po) and write its pixels.
-__device__ __forceinline__ void ps_fold(const KParams &P, const PsSlot &B, const float *scr) {
-    __threadfence();  // this wave's scratch stores are done; its loads below miss the stale L1
+// Fold a completed batch of npx pixels from px0 (all lanes of the wave call
+// it; lane po < npx owns pixel px0 + po) and write its pixels.
+__device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t npx, const float4 *c) {
+    // this wave's scratch stores complete before its loads below. Workgroup
+    // scope is enough (the same wave; the CU's L1 is coherent within a
+    // workgroup) and cheap: an agent-scope fence also writes back the L2.
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     const uint32_t po = threadIdx.x & 63u;
-    if (po >= B.npx) return;
-    const float *c0 = scr + (size_t)B.phys * 3 * P.ps_cap;
-    const float *c1 = c0 + P.ps_cap;
-    const float *c2 = c1 + P.ps_cap;
+    if (po >= npx) return;
     f3 acc = mk3(0.0f, 0.0f, 0.0f);
-    const uint32_t n = B.npx;
     uint32_t s = 0;
-    for (; s + 4 <= P.spp; s += 4) {  // four samples' loads in flight, adds in order
-        float x[4], y[4], z[4];
+    for (; s + 8 <= P.spp; s += 8) {  // eight samples' loads in flight, adds in order
+        float4 v[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t i = (s + k) * n + po;
-            x[k] = c0[i];
-            y[k] = c1[i];
-            z[k] = c2[i];
-        }
+        for (int k = 0; k < 8; ++k) v[k] = c[(s + k) * npx + po];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc = acc + mk3(x[k], y[k], z[k]);
+        for (int k = 0; k < 8; ++k) acc = acc + mk3(v[k].x, v[k].y, v[k].z);
     }
     for (; s < P.spp; ++s) {
-        const uint32_t i = s * n + po;
-        acc = acc + mk3(c0[i], c1[i], c2[i]);
+        const float4 v = c[s * npx + po];
+        acc = acc + mk3(v.x, v.y, v.z);
     }
-    output_pixel(P, B.px0 + po, acc);
+    output_pixel(P, px0 + po, acc);
 }
 
 template <bool kPF>
 __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
-    // dynamic LDS: [candidate list, list_bytes<kPF>][LDS copy of the spheres (n <= kCoopLds)]
+    // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][batch slots, kPsStateBytes]
+    //              [LDS copy of the spheres (n <= kCoopLds)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
     constexpr uint32_t kLB = list_bytes<kPF>();
-    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB);
+    float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
+    // this wave's batch slots: [k][0 px0, 1 npx, 2 items (0 = free), 3 items done]
+    uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
+    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes + kPsStateBytes);
     float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane < kPsSlots * 4) st[lane] = 0u;
     if (sph_lds) {
         for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
             s_pre4[i] = P.scene.pre4[i];
             s_rad[i] = P.scene.cen[i].w;
         }
-        __syncthreads();
     }
+    __syncthreads();
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
     const uint32_t wave = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
-    float *scr = P.ps_scratch + (size_t)wave * 6 * P.ps_cap;  // [phys slot][channel][ps_cap]
-    const uint32_t lane = threadIdx.x & 63u;
+    float4 *scr = reinterpret_cast<float4 *>(P.ps_scratch) + (size_t)wave * kPsSlots * P.ps_cap;  // [slot][ps_cap]
+    const unsigned long long t_start = P.wave_times ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long c_start = P.wave_times ? __builtin_amdgcn_s_memtime() : 0ull;
     PsLane L;
     L.active = false;
     L.segs = 0;
-    PsSlot A{0, 0, 0, 0, 0, 0, false}, B{1, 0, 0, 0, 0, 0, false};  // A: the slot being issued
+    // the slot being issued (wave-uniform): its slot index, first pixel, pixels, items, items issued
+    uint32_t cur = 0, c_px0 = 0, c_npx = 0, c_total = 0, c_issued = 0;
     bool exhausted = false;
     for (;;) {
-        // hand the idle lanes the next items: of batch A, then of a new batch
+        // hand the idle lanes the next items: of batch `cur`, then of a new batch
         for (int pass = 0; pass < 2; ++pass) {
             const uint64_t idle = __ballot(!L.active);
             if (idle == 0ull) break;
-            if (!A.live || A.issued == A.total) {
-                if (exhausted || B.live) break;
+            if (c_issued == c_total) {
+                if (exhausted) break;
+                const uint64_t freem = __ballot(lane < (uint32_t)kPsSlots && st[4 * lane + 2] == 0u);
+                if (freem == 0ull) break;  // every slot waits for its last samples
+                const uint32_t fk = (uint32_t)__builtin_ctzll(freem);
                 uint32_t base = 0;
                 if (lane == 0u) base = atomicAdd(P.queue, P.ps_px);
                 base = (uint32_t)__shfl((int)base, 0, 64);
@@ -1435,57 +1452,86 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
                     exhausted = true;
                     break;
                 }
-                B.live = true;
-                B.px0 = base;
-                B.npx = min(P.ps_px, npix - base);
-                B.total = B.npx * P.spp;
-                B.issued = 0;
-                B.done = 0;
-                const PsSlot t = A;
-                A = B;
-                B = t;
+                cur = fk;
+                c_px0 = base;
+                c_npx = min(P.ps_px, npix - base);
+                c_total = c_npx * P.spp;
+                c_issued = 0;
+                if (lane == 0u) {
+                    st[4 * fk + 0] = c_px0;
+                    st[4 * fk + 1] = c_npx;
+                    st[4 * fk + 3] = 0u;
+                    st[4 * fk + 2] = c_total;
+                }
             }
-            const uint32_t take = min((uint32_t)__popcll(idle), A.total - A.issued);
+            const uint32_t take = min((uint32_t)__popcll(idle), c_total - c_issued);
             const uint32_t rank =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            if (!L.active && rank < take) ps_start(P, F, A, A.issued + rank, L);
-            A.issued += take;
+            if (!L.active && rank < take) ps_start(P, F, c_px0, c_npx, cur, c_issued + rank, L);
+            c_issued += take;
         }
         if (__ballot(L.active) == 0ull) break;  // queue exhausted and every batch folded
         bool ended = false;
+        const uint64_t act = __ballot(L.active);
+        float best = __uint_as_float(0x7f800000u);
+        int hit = -1;
+        if (exhausted && __popcll(act) <= kCoopMax) {  // the wave's last few samples: group coop
+            __builtin_amdgcn_s_setprio(kTailPrio);
+            bool seq = false;
+            hit = sph_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, (const float *)s_rad, act, L.active,
+                                             L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list, best, seq)
+                          : hit_world_groups(P.scene, P.scene.pre4, (const float *)nullptr, act, L.active, L.o, L.d,
+                                             L.a, L.inv_a, kTMin, coop_ws, list, best, seq);
+            if (L.active && seq) {  // a non-finite root in the group: the exact path
+                best = __uint_as_float(0x7f800000u);
+                hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+            }
+        } else if (L.active) {
+            hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene,
+                                                  [s_pre4, s_rad](uint32_t i) {
+                                                      const float4 c = s_pre4[i];
+                                                      return make_float4(c.x, c.y, c.z, s_rad[i]);
+                                                  },
+                                                  L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                          : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+        }
         if (L.active) {
-            float best = __uint_as_float(0x7f800000u);
-            const int hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene,
-                                                            [s_pre4, s_rad](uint32_t i) {
-                                                                const float4 c = s_pre4[i];
-                                                                return make_float4(c.x, c.y, c.z, s_rad[i]);
-                                                            },
-                                                            L.o, L.d, L.a, L.inv_a, kTMin, best, list)
-                                    : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             L.segs++;
             f3 c = mk3(0.0f, 0.0f, 0.0f);
             const int r = path_segment(P, L, min(hit, last), best, c);
             if (r != kSegContinue) {
-                float *o = scr + (size_t)L.slot * 3 * P.ps_cap + L.sidx;
-                o[0] = c.x;  // +0 for a black path
-                o[P.ps_cap] = c.y;
-                o[2 * P.ps_cap] = c.z;
+#if RTX_PS_DIAG_NOSTORE  // timing diagnostic only: WRONG images
+                if (c.x == 12345.0f)
+#endif
+                scr[(size_t)L.slot * P.ps_cap + L.sidx] = make_float4(c.x, c.y, c.z, 0.0f);  // +0: black path
+                atomicAdd(&st[4 * L.slot + 3], 1u);
                 L.active = false;
                 ended = true;
             }
         }
-        A.done += (uint32_t)__popcll(__ballot(ended && L.slot == A.phys));
-        B.done += (uint32_t)__popcll(__ballot(ended && L.slot == B.phys));
-        if (A.live && A.done == A.total) {
-            ps_fold(P, A, scr);
-            A.live = false;
-        }
-        if (B.live && B.done == B.total) {
-            ps_fold(P, B, scr);
-            B.live = false;
+        if (__ballot(ended) == 0ull) continue;
+        // fold every batch whose samples are all done
+        uint64_t full = __ballot(lane < (uint32_t)kPsSlots && st[4 * lane + 2] != 0u &&
+                                 st[4 * lane + 3] == st[4 * lane + 2]);
+        while (full != 0ull) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(full);
+            full &= full - 1ull;
+            ps_fold(P, st[4 * k + 0], st[4 * k + 1], scr + (size_t)k * P.ps_cap);
+            if (lane == 0u) st[4 * k + 2] = 0u;
         }
     }
+    uint32_t wsegs = L.segs;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wsegs += __shfl_xor(wsegs, off, 64);
     count_segments(P, L.segs);
+    // diagnostic only (rtx_debug_wave_times, armed with 2 x waves): per wave
+    // (start, end) s_memrealtime, then (shader clocks, segments) in the upper half
+    if (P.wave_times && lane == 0u && wave < P.wave_cap / 2) {
+        P.wave_times[2 * wave] = t_start;
+        P.wave_times[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+        P.wave_times[P.wave_cap + 2 * wave] = __builtin_amdgcn_s_memtime() - c_start;
+        P.wave_times[P.wave_cap + 2 * wave + 1] = wsegs;
+    }
 }
 
 // spp == 0 or depth == 0: no segment is traced; the pixel is
@@ -1588,17 +1634,34 @@ inline uint32_t ceil_div(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1)
 }  // namespace
 
 // Workgroups the device keeps resident for `kern` (per-CU occupancy x CUs),
-// queried once per kernel/LDS size. Over-estimating is harmless: extra
-// workgroups find the pixel queue drained and exit.
+// queried once per (device, kernel, LDS size) and cached: the occupancy query
+// costs host time inside every launch's timed region otherwise. Over-
+// estimating is harmless: extra workgroups find the queue drained and exit.
 static uint32_t resident_blocks(const void *kern, size_t lds) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 1024;
+    struct Entry {
+        int dev;
+        const void *kern;
+        size_t lds;
+        uint32_t blocks;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (const Entry &e : cache)
+            if (e.dev == dev && e.kern == kern && e.lds == lds) return e.blocks;
+    }
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)kRB, lds) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
-    return (uint32_t)(cus * per_cu);
+    const uint32_t blocks = (uint32_t)(cus * per_cu);
+    std::lock_guard<std::mutex> g(mu);
+    cache.push_back(Entry{dev, kern, lds, blocks});
+    return blocks;
 }
 
 // Dynamic LDS above 64 KiB must be opted into per kernel.
@@ -1640,40 +1703,49 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Per-sample launches: items per batch slot. A batch is ps_px pixels with
-// ps_px * spp <= ps_cap items; about 8 batches per resident wave keep the
-// waves balanced at the end of a frame share.
-constexpr uint32_t kPsItems = 4096;
+// Per-sample launches: items per batch slot (ps_cap = max(kPsItems, spp)); a
+// batch is at most ps_px pixels, ps_px * spp <= ps_cap.
+#ifndef RTX_PS_ITEMS
+#define RTX_PS_ITEMS 512
+#endif
+constexpr uint32_t kPsItems = RTX_PS_ITEMS;
+#ifndef RTX_PS_BPW
+#define RTX_PS_BPW 40
+#endif
+constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() : kListBytes) +
+    return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
            (!use_pf(s) && s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
 }
 static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }
 static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
+// Every resident wave (an item is a sample, not a pixel: a frame share with
+// fewer pixels than lanes still fills the GPU), fewer only for tiny frames.
 static uint32_t ps_waves(const KParams &p) {
     const bool pf = use_pf(p.scene);
-    const uint32_t npix = p.rows_local * p.width;
-    const uint32_t blocks = min(ceil_div(npix, kRB), resident_blocks(ps_fn(pf), ps_lds(p.scene)));
+    const uint64_t items = (uint64_t)p.rows_local * p.width * p.spp;
+    const uint32_t blocks = min(ceil_div(items, kRB), resident_blocks(ps_fn(pf), ps_lds(p.scene)));
     return blocks * (kRB / 64);
 }
 size_t ps_scratch_floats(const KParams &p) {
     if (p.rng_mode != 1u || p.spp == 0 || p.depth == 0 || (uint64_t)p.rows_local * p.width == 0) return 0;
-    return (size_t)ps_waves(p) * 6 * ps_cap_of(p.spp);
+    return (size_t)ps_waves(p) * kPsSlots * 4 * ps_cap_of(p.spp);
 }
 static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_t stream) {
     const bool pf = use_pf(p.scene);
     const size_t lds = ps_lds(p.scene);
     hipError_t e = allow_lds(ps_fn(pf), lds);
     if (e != hipSuccess) return e;
-    const uint32_t npix = p.rows_local * p.width;
     const uint32_t waves = ps_waves(p);
     KParams q = p;
     q.ps_cap = ps_cap_of(p.spp);
     q.ps_scratch = sched.ps_scratch;
-    if (!q.ps_scratch || sched.ps_floats < (size_t)waves * 6 * q.ps_cap) return hipErrorInvalidValue;
-    const uint64_t items = (uint64_t)npix * p.spp;
-    const uint64_t target = std::min<uint64_t>(std::max<uint64_t>(items / ((uint64_t)waves * 8u), 64u), kPsItems);
-    q.ps_px = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(64u, target / p.spp));
+    if (!q.ps_scratch || sched.ps_floats < (size_t)waves * kPsSlots * 4 * q.ps_cap) return hipErrorInvalidValue;
+    // batches of <= ps_cap items, and about kPsBatchesPerWave of them per
+    // wave for a small frame share (the waves then finish together)
+    const uint64_t per_wave = (uint64_t)p.rows_local * p.width * p.spp / std::max(waves, 1u);
+    const uint64_t items = std::min<uint64_t>(q.ps_cap, per_wave / kPsBatchesPerWave);
+    q.ps_px = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(64u, items / p.spp));
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint32_t blocks = waves / (kRB / 64);

@@ -37,7 +37,7 @@ for path in a.libs or [None]:
     buf = ctx.alloc((H, W, 4))
     t1 = None
     for R in a.parts:
-        times = []
+        times, segs = [], []
         for p in range(R):
             ctx.render_rows(a.tile_rows, p, R, buf.ptr)  # warm
             ctx.sync()
@@ -46,12 +46,13 @@ for path in a.libs or [None]:
                 ctx.render_rows(a.tile_rows, p, R, buf.ptr)
             st = ctx.stats()
             times.append(st.kernel_ms / st.launches)
+            segs.append(st.segments // st.launches)
         crit = max(times)
         if R == 1:
             t1 = crit
         rep = {"lib": os.path.basename(path) if path else "default", "rng": a.rng, "parts": R,
                "part_ms": [round(t, 3) for t in times], "critical_ms": round(crit, 3),
-               "mean_ms": round(sum(times) / R, 3)}
+               "mean_ms": round(sum(times) / R, 3), "part_segments": segs}
         if t1:
             rep["efficiency"] = round(t1 / (R * crit), 4)
         print(json.dumps(rep), flush=True)

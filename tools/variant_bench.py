@@ -25,6 +25,7 @@ ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--grid", type=int, default=11)
 ap.add_argument("--max-spheres", type=int, default=0)
+ap.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
 ap.add_argument("names", nargs="*")
 a = ap.parse_args()
 
@@ -34,6 +35,7 @@ if a.names:
     paths = [os.path.join(vdir, f"librtx_{n}.so") for n in a.names]
 world = rtx.random_world(a.grid, capacity=a.max_spheres or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(a.width, a.height, aspect=a.width / a.height)
+frame.rng_mode = 1 if a.rng == "per-sample" else 0
 ctxs = {}
 for p in paths:
     name = os.path.basename(p)[len("librtx_"):-3]
@@ -61,7 +63,7 @@ for r in range(a.rounds):
             if ref is None:
                 ref = img
             same = (img.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(img) & np.isnan(ref))
-            if not same.all() and "diag" not in n:
+            if not same.all() and "diag" not in n and "nostore" not in n:
                 print(json.dumps({"variant": n, "ERROR": f"{(~same).sum()} values differ from first variant"}))
         print(json.dumps({"variant": n, "round": r, "kernel_ms": round(times[n][-1], 3),
                           "wall_ms": round(wall * 1e3, 3),
