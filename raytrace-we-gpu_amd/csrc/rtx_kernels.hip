@@ -1257,14 +1257,15 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // Positions: bucket start (prefix of the global counts) + a range the
 // block reserves in the bucket + the element's rank inside the block. The
 // order within a bucket is arbitrary; per-pixel results do not depend on it.
+// (Tile-major order within a bucket measured no faster: DESIGN.md §7.)
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          const uint32_t *counts, uint32_t *cursors,
                                                          uint32_t *perm) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
-    const uint32_t n = width * rows;
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
+    const uint32_t n = width * rows;
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
