@@ -124,10 +124,11 @@ def pmc_traffic(args):
 
 
 SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU",
-               "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+               "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS",
+               "GRBM_GUI_ACTIVE"]
 
 
-def pmc_valu(args, n_cu):
+def pmc_valu(args, n_cu, launch_ms):
     """Executed-work view of the render launch (its own --pmc pass): how busy
     the VALU issue was and how many lanes each VALU instruction had.
     SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8
@@ -138,10 +139,16 @@ def pmc_valu(args, n_cu):
         return {"skipped": str(e)}
     cycles = v["GRBM_GUI_ACTIVE"] / 8.0
     simds = 4 * n_cu
-    return {"valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
+    flops = v["SQ_INSTS_VALU_FLOPS_FP32"] + v["SQ_INSTS_VALU_FLOPS_FP32_TRANS"]
+    tflops = flops / (launch_ms * 1e-3) / 1e12
+    return {"executed_tflops": round(tflops, 3), "executed_frac": round(tflops / FP32_PEAK_TFLOPS, 4),
+            "executed_flop_per_launch": flops,
+            "valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
             "valu_lane_util": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
             "valu_insts_per_simd_cycle": round(v["SQ_INSTS_VALU"] / (simds * cycles), 4),
-            "formula": "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8); "
+            "formula": "executed = (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS) / launch time (the FP32 FLOPs the "
+                       "VALU actually ran, prefilter and exact tests and shading included); "
+                       "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8) (rocprof VALUBusy); "
                        "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)",
             "counters": v, "cus": n_cu}
 
@@ -285,7 +292,7 @@ def main():
         traffic, pmc_note, executed = (None, "skipped", None)
         if args.pmc == "auto" and R == 1:
             traffic, pmc_note = pmc_traffic(args)
-            executed = pmc_valu(args, torch.cuda.get_device_properties(local_rank).multi_processor_count)
+            executed = pmc_valu(args, torch.cuda.get_device_properties(local_rank).multi_processor_count, launch_ms)
         host_img = image.cpu().numpy() if R == 1 else None
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
