@@ -139,15 +139,20 @@ def pmc_valu(args, n_cu, launch_ms):
         return {"skipped": str(e)}
     cycles = v["GRBM_GUI_ACTIVE"] / 8.0
     simds = 4 * n_cu
-    flops = v["SQ_INSTS_VALU_FLOPS_FP32"] + v["SQ_INSTS_VALU_FLOPS_FP32_TRANS"]
+    # the FLOPS counters count per wave-instruction (FMA 2, ...): x64 lanes is
+    # rocprof's convention; x the measured lane utilisation counts active lanes
+    lane_util = v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"])
+    flops = 64.0 * (v["SQ_INSTS_VALU_FLOPS_FP32"] + v["SQ_INSTS_VALU_FLOPS_FP32_TRANS"])
     tflops = flops / (launch_ms * 1e-3) / 1e12
     return {"executed_tflops": round(tflops, 3), "executed_frac": round(tflops / FP32_PEAK_TFLOPS, 4),
+            "executed_tflops_active_lanes": round(tflops * lane_util, 3),
             "executed_flop_per_launch": flops,
             "valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
             "valu_lane_util": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
             "valu_insts_per_simd_cycle": round(v["SQ_INSTS_VALU"] / (simds * cycles), 4),
-            "formula": "executed = (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS) / launch time (the FP32 FLOPs the "
-                       "VALU actually ran, prefilter and exact tests and shading included); "
+            "formula": "executed = 64 * (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS) / launch time (the FP32 FLOPs "
+                       "the VALU ran, prefilter, exact tests and shading included; _active_lanes scales by "
+                       "valu_lane_util); "
                        "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8) (rocprof VALUBusy); "
                        "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)",
             "counters": v, "cus": n_cu}
