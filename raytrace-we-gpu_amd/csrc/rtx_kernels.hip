@@ -92,6 +92,8 @@ constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
 constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha * a lane's share of the summed keys
 constexpr double kHeavy1Alpha = 1.7;    // tier 1 iff key > alpha1 * share
 constexpr double kHeavy1AlphaSmall = 4.0;   // the same for a small frame share
+constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than this * resident lanes
+constexpr double kHeavy1AlphaLow = 3.5;     // tier-1 bar for a low share
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 constexpr double kHeavy2AlphaMedium = 1.5;  // tier 2 for a medium share: key > this * share
@@ -1306,7 +1308,11 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     for (uint32_t b = 0; b < kCostBuckets; ++b) w += (double)counts[b] * (double)(kCostBuckets - 1u - b);
     const double share = w / (double)(lanes ? lanes : 1u);
     const bool small = (double)npix < kHeavyRho * (double)lanes;
-    const double a1 = small ? kHeavy1AlphaSmall : kHeavy1Alpha;
+    // fewer than kHeavyRhoLow pixels per lane (a 4-way split of C2): tier 1
+    // only above kHeavy1AlphaLow x share — one-ray waves are expensive, and
+    // at this share there are many candidates that crowd the SIMDs
+    const bool low = !small && (double)npix < kHeavyRhoLow * (double)lanes;
+    const double a1 = small ? kHeavy1AlphaSmall : low ? kHeavy1AlphaLow : kHeavy1Alpha;
     // a medium share (fewer than kHeavyRho2 pixels per lane, e.g. a
     // 2- or 4-way split) also gets tier 2 above kHeavy2AlphaMedium x share
     const bool medium = !small && (double)npix < kHeavyRho2 * (double)lanes;
