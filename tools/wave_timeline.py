@@ -17,11 +17,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
 ap.add_argument("--parts", type=int, default=1)
 ap.add_argument("--part", type=int, default=0)
+ap.add_argument("--grid", type=int, default=11)
+ap.add_argument("--cap", type=int, default=0)
+ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("lib", nargs="?")
 a = ap.parse_args()
 lib = rtx.load_library(a.lib) if a.lib else None
 W_, H_, T_ = 1920, 1080, 5
-world = rtx.random_world(11, depth=50, spp=100)
+world = rtx.random_world(a.grid, capacity=a.cap or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W_, H_)
 frame.rng_mode = 1 if a.rng == "per-sample" else 0
 ctx = rtx.Context(0, lib=lib)
