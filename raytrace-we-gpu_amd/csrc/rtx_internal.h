@@ -57,7 +57,8 @@ struct KParams {
     uint32_t wave_cap;             // pairs in wave_times
     const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
-    float4 *state;                 // per pixel (acc, seed) after kCostSpp samples: written by the
+    uint32_t cost_spp;             // samples the pre-pass traced (the render resumes after them)
+    float4 *state;                 // per pixel (acc, seed) after cost_spp samples: written by the
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
@@ -84,6 +85,7 @@ struct KSchedule {
 };
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
+constexpr uint32_t kCostSppLarge = 1;  // ... for scenes above kScanPfMin spheres (C5: 1,997 vs 2,018 ms)
 constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
 constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)
 

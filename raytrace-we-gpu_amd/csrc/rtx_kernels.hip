@@ -971,10 +971,10 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
     L.gid = gid;
     lane_pixel(P, gid, L.x, L.y);
     L.seg0 = L.segs;
-    if (P.state && !P.cost_out) {  // after the pre-pass's kCostSpp samples (identical state)
+    if (P.state && !P.cost_out) {  // after the pre-pass's cost_spp samples (identical state)
         const float4 st = P.state[gid];
         L.acc = mk3(st.x, st.y, st.z);
-        L.sample = kCostSpp;
+        L.sample = P.cost_spp;
         L.seed = st.w;
     } else {
         L.acc = mk3(0.0f, 0.0f, 0.0f);
@@ -1241,7 +1241,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
 // key is the sum over a (2R+1)^2 window of neighbouring pixels (clamped
 // at the edges), which averages that noise over similar pixels.
 constexpr int kLptRadius = 1;  // 3x3 window (radius 0 was 36 % slower, radius 2 5 % slower)
-__device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, uint32_t width, uint32_t rows) {
+__device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, uint32_t width, uint32_t rows,
+                                             uint32_t cost_spp) {
     const int x = (int)(i % width), y = (int)(i / width);
     uint32_t sum = 0;
     for (int dy = -kLptRadius; dy <= kLptRadius; ++dy) {
@@ -1252,14 +1253,14 @@ __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, u
         }
     }
     // scaled to 9 one-sample costs (the 3x3, 1-spp key the tiers were tuned on)
-    constexpr uint32_t kWin = (2 * kLptRadius + 1) * (2 * kLptRadius + 1) * kCostSpp;
-    if (kWin != 9u) sum = (sum * 9u + kWin / 2u) / kWin;
+    const uint32_t win = (2 * kLptRadius + 1) * (2 * kLptRadius + 1) * cost_spp;
+    if (win != 9u) sum = (sum * 9u + win / 2u) / win;
     return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
 }
 constexpr uint32_t kSortPerThread = 16;
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
-                                                      uint32_t *counts) {
+                                                      uint32_t cost_spp, uint32_t *counts) {
     __shared__ uint32_t h[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -1267,7 +1268,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows)], 1u);
+        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp)], 1u);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
@@ -1279,6 +1280,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // order within a bucket is arbitrary; per-pixel results do not depend on it.
 // (Tile-major order within a bucket measured no faster: DESIGN.md §7.)
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
+                                                         uint32_t cost_spp,
                                                          const uint32_t *counts, uint32_t *cursors,
                                                          uint32_t *perm) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
@@ -1289,7 +1291,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        key[k] = i < n ? cost_key(cost, i, width, rows) : 0u;
+        key[k] = i < n ? cost_key(cost, i, width, rows, cost_spp) : 0u;
         rank[k] = i < n ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
     __syncthreads();
@@ -1805,7 +1807,9 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     // 1. cost pre-pass: kCostSpp samples per pixel; records each pixel's
     // segments and its state (acc, seed) after them, which the render resumes
     KParams c = p;
-    c.spp = min(p.spp, kCostSpp);
+    // large scenes: one sample — there a segment costs ~4 ms of wave time and
+    // the pre-pass waits on its heaviest pixel's chain
+    c.spp = min(p.spp, pf ? kCostSppLarge : kCostSpp);
     c.cost_out = sched.cost;
     c.state = sched.state;
     c.accum = nullptr;
@@ -1828,15 +1832,16 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     // 2. counting sort by cost, descending
     const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, sched.buckets);
+                       p.rows_local, c.spp, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
     const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
+                       p.rows_local, c.spp, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
     KParams q = p;
+    q.cost_spp = c.spp;
     q.perm = sched.perm;
     q.state = sched.state;
     q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * kPrioFracX100 / 100u);
