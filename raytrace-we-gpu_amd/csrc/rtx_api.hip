@@ -50,6 +50,10 @@ constexpr size_t kEventRing = 64;
 
 }  // namespace
 
+#ifndef RTX_FLAT
+#define RTX_FLAT 1
+#endif
+
 struct rtx_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -59,6 +63,8 @@ struct rtx_ctx {
     float *d_pre = nullptr;  // prefilter blocks (rtx_prefilter.h)
     float4 *d_pre4 = nullptr;  // prefilter data per sphere (tail coop)
     float smag = 0.0f;
+    float flat_cy = 0.0f;  // scene's flat run of `pre` blocks (rtx_internal.h KScene)
+    uint32_t flat_lo = 0, flat_hi = 0;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
@@ -121,6 +127,9 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.pre = c->d_pre;
     s.pre4 = c->d_pre4;
     s.smag = c->smag;
+    s.flat_cy = c->flat_cy;
+    s.flat_lo = c->flat_lo;
+    s.flat_hi = c->flat_hi;
     s.cen = c->d_cen;
     s.mtype = c->d_mtype;
     s.mval = c->d_mval;
@@ -262,6 +271,29 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     }
     float smag_f = (float)smag;
     if ((double)smag_f < smag) smag_f = std::nextafter(smag_f, INFINITY);
+    // The longest run of flat blocks (rtx_prefilter.h: all 8 centre heights
+    // equal, bit for bit, and equal along the run): the scan's 6-op test.
+    uint32_t flat_lo = 0, flat_hi = 0;
+    float flat_cy = 0.0f;
+    {
+        auto bits = [&](uint32_t b, int k) { return __builtin_bit_cast(uint32_t, pre[32 * (size_t)b + 8 + k]); };
+        auto flat = [&](uint32_t b) {
+            for (int k = 1; k < 8; ++k)
+                if (bits(b, k) != bits(b, 0)) return false;
+            return true;
+        };
+        const uint32_t nblk = RTX_FLAT ? n_pad / 8 : 0;  // RTX_FLAT=0: A/B build without flat runs
+        for (uint32_t b = 0; b < nblk;) {
+            if (!flat(b)) {
+                ++b;
+                continue;
+            }
+            uint32_t e = b + 1;
+            while (e < nblk && flat(e) && bits(e, 0) == bits(b, 0)) ++e;
+            if (e - b > flat_hi - flat_lo) flat_lo = b, flat_hi = e, flat_cy = pre[32 * (size_t)b + 8];
+            b = e;
+        }
+    }
     for (uint32_t i = 0; i < n; ++i) {
         cen[i] = make_float4(w->spheres[4 * i + 0], w->spheres[4 * i + 1], w->spheres[4 * i + 2],
                              w->spheres[4 * i + 3]);
@@ -296,6 +328,9 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     c->n = n;
     c->n_pad = n_pad;
     c->smag = smag_f;
+    c->flat_cy = flat_cy;
+    c->flat_lo = flat_lo;
+    c->flat_hi = flat_hi;
     c->depth = w->depth;
     c->spp = w->spp;
     c->have_world = true;

@@ -21,7 +21,9 @@ namespace rtx {
 //                         prefilter's inflated r^2 (rtx_prefilter.h) — the
 //                         array every ray segment scans
 // `smag` bounds |c| + r over the scene (rounded up), for the prefilter's
-// per-ray overflow guard.
+// per-ray overflow guard. Blocks [flat_lo, flat_hi) of `pre` hold spheres
+// whose centres all have height flat_cy (the scan's 6-op test,
+// rtx_prefilter.h line_test_q_flat).
 struct KScene {
     const float *soa;
     const float *pre;
@@ -31,6 +33,8 @@ struct KScene {
     const float4 *mval;
     uint32_t n, n_pad;
     float smag;
+    float flat_cy;             // centre height shared by every sphere of blocks [flat_lo, flat_hi)
+    uint32_t flat_lo, flat_hi;  // the scene's longest run of such flat blocks (empty: 0, 0)
 };
 
 constexpr uint32_t kPad = 8;  // spheres per AoSoA block

@@ -241,13 +241,14 @@ __device__ __forceinline__ void sload_blk(cfloat_p p, f16v &lo, f16v &hi, f2v &d
 __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(lo), "+s"(hi));
 }
-template <bool kPF>
-__device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk,
-                                                   const LineTest &T, uint32_t *list, uint32_t &cnt) {
-    cnt = 0;
-    uint32_t *my = list + threadIdx.x;
+// One run of blocks [b, end), all flat (kFlat: the 6-op test, kvn = kv)
+// or not (kvn = -(o.v)). Returns the block to resume at; `full` when it
+// stopped because some lane's list is full.
+template <bool kPF, bool kFlat>
+__device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_t end, const LineTest &T,
+                                               float kvn1, uint32_t *my, uint32_t &cnt, bool &full) {
     f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
-    f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
+    f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, kvn = {kvn1, kvn1};
     const f2v th = {T.thr, T.thr};
     // One 8-sphere block (blk(i) = its i-th float); true when some lane's
     // list is full and the scan must stop after this block.
@@ -256,11 +257,16 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const f2v cx = {blk(2 * p), blk(2 * p + 1)};
-            const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
             const f2v cz = {blk(16 + 2 * p), blk(17 + 2 * p)};
             const f2v R = {blk(24 + 2 * p), blk(25 + 2 * p)};
             const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
-            const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
+            f2v pv;
+            if constexpr (kFlat) {
+                pv = fma2(cx, vx, fma2(cz, vz, kvn));
+            } else {
+                const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
+                pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, kvn)));
+            }
             q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
         }
         // a chain, so that it folds into v_max3_f32
@@ -286,31 +292,56 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
         }
         return false;
     };
+    full = true;
     if constexpr (kPF) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
-        if (b >= nblk) return nblk;
         f16v a_lo, a_hi, b_lo, b_hi;
-        sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
+        sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
         sload_wait(a_lo, a_hi);
         for (;;) {
-            sload_blk(pre + 32 * min(b + 1, nblk - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, nov);
-            bool full = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
+            sload_blk(pre + 32 * min(b + 1, end - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, kvn);
+            bool f = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
             sload_wait(b_lo, b_hi);
-            if (full) return b + 1;
-            if (++b >= nblk) return nblk;
-            sload_blk(pre + 32 * min(b + 1, nblk - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, nov);
-            full = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
+            if (f) return b + 1;
+            if (++b >= end) break;
+            sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
+            f = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
             sload_wait(a_lo, a_hi);
-            if (full) return b + 1;
-            if (++b >= nblk) return nblk;
+            if (f) return b + 1;
+            if (++b >= end) break;
         }
     } else {
-        for (; b < nblk; ++b) {
+        for (; b < end; ++b) {
             const cfloat_p blk = pre + 32 * b;
             if (step([&](int i) { return blk[i]; }, b)) return b + 1;
         }
-        return nblk;
     }
+    full = false;
+    return end;
+}
+
+// The scan over blocks [b, nblk): the scene's flat run [flat_lo, flat_hi)
+// (rtx_internal.h KScene) with the 6-op test, the rest with the 7-op one.
+// Returns the block to resume at: nblk, or earlier once some lane's list is
+// full (wave-uniform).
+template <bool kPF>
+__device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk, const LineTest &T,
+                                                   const KScene &S, uint32_t *list, uint32_t &cnt) {
+    cnt = 0;
+    uint32_t *my = list + threadIdx.x;
+    const float kv = line_test_kv(T, S.flat_cy);
+    while (b < nblk) {
+        bool full;
+        if (b < S.flat_lo) {
+            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nov, my, cnt, full);
+        } else if (b < S.flat_hi) {
+            b = scan_range<kPF, true>(pre, b, S.flat_hi, T, kv, my, cnt, full);
+        } else {
+            b = scan_range<kPF, false>(pre, b, nblk, T, T.nov, my, cnt, full);
+        }
+        if (full) break;
+    }
+    return b;
 }
 
 // Resolve the lane's list (m entries: first sphere index | mask << 24)
@@ -409,7 +440,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = scan_prefilter<kPF>(pre, b, nblk, T, list, cnt);
+        b = scan_prefilter<kPF>(pre, b, nblk, T, S, list, cnt);
         ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
     } while (b < nblk);
     if (!ok) {

@@ -107,4 +107,18 @@ RTX_HD float line_test_q(const LineTest &T, float cx, float cy, float cz, float 
     return fmaf(-pv, pv, fmaf(-pu, pu, R));
 }
 
+// Flat blocks: all 8 spheres of a block share one centre height cy (the
+// RTIOW scenes' small spheres all sit at y = 0.2). The cy term of c.v is
+// then one per-ray value, kv = fl(cy*vy - o.v), computed once per segment,
+// and a test costs 6 fp32 ops instead of 7. c.v - o.v is still a chain of
+// three fma over the same four terms (cy*vy first instead of second), so
+// the rounding bound of that chain (6u S) and the margins above are
+// unchanged; tests/prefilter_check.cpp checks both orders.
+RTX_HD float line_test_kv(const LineTest &T, float cy) { return fmaf(cy, T.vy, T.nov); }
+RTX_HD float line_test_q_flat(const LineTest &T, float kv, float cx, float cz, float R) {
+    const float pu = fmaf(cx, T.ux, fmaf(cz, T.uz, T.nou));
+    const float pv = fmaf(cx, T.vx, fmaf(cz, T.vz, kv));
+    return fmaf(-pv, pv, fmaf(-pu, pu, R));
+}
+
 }  // namespace rtx

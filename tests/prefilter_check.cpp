@@ -5,7 +5,8 @@
 // rays, far origins, centre magnitudes 1e-2 .. 1e4, radii 1e-3 .. 1e3 —
 // whenever the reference's fp32 discriminant is >= 0 or NaN
 // (ShaderCompute.hlsl:158-166; the op order of oracle/rtx_oracle.c
-// hit_world32), the prefilter must flag the sphere.
+// hit_world32), the prefilter must flag the sphere — in both op orders the
+// scan uses (line_test_q, and line_test_q_flat for flat blocks).
 // Prints one JSON line; exit status 1 if any reference candidate is missed.
 // Build: g++ -O2 -std=c++17 -ffp-contract=off -mfma prefilter_check.cpp
 #include <cmath>
@@ -92,9 +93,11 @@ int main(int argc, char **argv) {
         const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
         const float R = rtx::prefilter_R(c[0], c[1], c[2], r2);
         const float q = rtx::line_test_q(T, c[0], c[1], c[2], R);
+        // the flat-block order (cy*vy first), as the scan runs it on flat blocks
+        const float qf = rtx::line_test_q_flat(T, rtx::line_test_kv(T, c[1]), c[0], c[2], R);
         const float disc = ref_disc(o, d, c, -r2, a);
         const bool ref = !(disc < 0.0f);
-        const bool flag = !(q < T.thr);
+        const bool flag = !(q < T.thr) && !(qf < T.thr);
         ref_pos += ref;
         flagged += flag;
         false_pos += flag && !ref;
@@ -106,7 +109,7 @@ int main(int argc, char **argv) {
         }
         if (ref && T.thr != -INFINITY) {
             // share of the margin the rounding errors used: (estimated dperp^2 - r^2) / (R - thr - r^2)
-            const double used = (((double)R - q) - r2) / ((double)R - T.thr - r2);
+            const double used = (((double)R - std::fmin(q, qf)) - r2) / ((double)R - T.thr - r2);
             if (used > max_used) max_used = used;
         }
     }

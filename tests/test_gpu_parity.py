@@ -631,6 +631,35 @@ def test_scan_kernel_choice_boundary(gpu_ctx, oracle, rtx):
         assert st.segments == segs
 
 
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+@pytest.mark.parametrize("ext", [11, 20])
+def test_flat_block_runs_bit_exact(request, oracle, rtx, ctx_name, ext):
+    """The scan's 6-op test on the scene's longest run of flat blocks (all 8
+    centres at one height, rtx_prefilter.h line_test_q_flat) and the 7-op
+    test elsewhere: a RTIOW scene broken into several runs — two blocks with
+    mixed heights, one flat block at another height, a mixed last block —
+    on both scan kernels (486 and 1,600 spheres) and the stress build (scan
+    rounds that stop and resume inside and across runs)."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(ext, depth=50, spp=8)
+    s = world.spheres
+    s[100:108, 1] = np.float32(0.35)  # blocks 12 and 13 become mixed
+    s[200:208, 1] = np.float32(0.35)  # block 25: flat at another height
+    s[-1, 1] = np.float32(0.5)        # the last block (padded with copies of n-1) mixed
+    rng = np.random.default_rng(3)
+    rays = np.concatenate([grazing_rays(s, 12000, rng, ext_frac=0.02),
+                           np.concatenate([rng.uniform(-12, 12, (4000, 1)), rng.uniform(0.05, 3, (4000, 1)),
+                                           rng.uniform(-12, 12, (4000, 1)), rng.normal(size=(4000, 3))], 1)
+                           .astype(np.float32)])
+    ctx.upload_world(world)
+    assert_bits_equal(ctx.debug_hit_world(rays), oracle.hit_world_f32(world, rays), f"{ctx_name} n={world.count}")
+    frame = rtx.camera_look_at(64, 36, aspect=64 / 36)
+    img, st = render_gpu(ctx, world, frame)
+    want, segs = oracle.render_rows(world, frame, np.arange(36), nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img, want, f"{ctx_name} n={world.count} frame")
+    assert st.segments == segs
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""
