@@ -45,9 +45,10 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best noflat prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psnostore psb80 psb20
+VARIANTS := best noflat ieeebasis prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psnostore psb80 psb20
 VFLAGS_best          :=
 VFLAGS_noflat        := -DRTX_FLAT=0
+VFLAGS_ieeebasis     := -DRTX_IEEE_BASIS=1
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1

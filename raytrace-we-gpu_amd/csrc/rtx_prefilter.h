@@ -21,12 +21,16 @@
 // Error bound (u = unit roundoff 2^-24, S = |c| + |o|):
 //   reference disc rounding, divided by a:    13|oc|^2 + 7r^2
 //   oc = fl(o - c) perturbation:               2|oc|^2
-//   basis (u, v) error (<= 4u, 9u per vector): 20|oc|^2
+//   basis (u, v) error (<= 4u, 10u per vector): 23|oc|^2
 //   c.u - o.u, c.v - o.v chains (4u S, 6u S):  15 S^2
 //   final two fma:                              4r^2
-//   total <= u (50 S^2 + 11 r^2) <= u (100|c|^2 + 100|o|^2 + 11 r^2)
+//   total <= u (53 S^2 + 11 r^2) <= u (106|c|^2 + 106|o|^2 + 11 r^2)
+// The basis is built with the 1-ulp hardware reciprocal square root
+// (v_rsq_f32: 1/|(dx, dz)| and 1/|d|), not IEEE sqrt and division: it only
+// has to be close to orthonormal, its error is in the bound above, and it
+// saves ~55 VALU instructions per ray segment.
 // The margins below are 1.6e-5 (= 268u) per |c|^2 and |o|^2 and 2e-6
-// (= 33u) per r^2, i.e. >= 2.6x that bound, plus an absolute 1e-24 that
+// (= 33u) per r^2, i.e. >= 2.5x that bound, plus an absolute 1e-24 that
 // covers subnormal rounding in the region the per-lane `safe` test admits
 // (a in [2^-40, 2^40], ray not within ~2^-20 rad of vertical, no fp32
 // overflow). Lanes outside that region get u = v = 0 and thr = -inf: every
@@ -66,6 +70,22 @@ inline float prefilter_R(float cx, float cy, float cz, float r2) {
     return f;
 }
 
+// The two hardware approximations of the basis: v_rsq_f32 and v_sqrt_f32
+// (1 ulp). The host build (tests/prefilter_check.cpp) models them as the
+// correctly rounded value moved by pf_host_ulp[k] ulps (-1, 0, +1), set per
+// case by the checker.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float pf_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float pf_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+#else
+inline int pf_host_ulp[3] = {0, 0, 0};
+inline float pf_nudge(float v, int k) {
+    return k > 0 ? nextafterf(v, INFINITY) : k < 0 ? nextafterf(v, -INFINITY) : v;
+}
+inline float pf_rsq_k(float x, int k) { return pf_nudge((float)(1.0 / sqrt((double)x)), pf_host_ulp[k]); }
+inline float pf_sqrt(float x) { return pf_nudge((float)sqrt((double)x), pf_host_ulp[2]); }
+#endif
+
 // Ray side, once per segment. `a` is the reference's |d|^2 (fma form),
 // `smag` an upper bound of |c| + r over the scene (rtx_upload_world).
 RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy, float dz, float a,
@@ -76,7 +96,7 @@ RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy
     // a in [2^-40, 2^40]; d not within ~2^-20 rad of the y axis; S = smag +
     // |o| with S^2 and a*S^2 <= 1e36 (no fp32 overflow in disc or Q).
     // NaN or infinite inputs fail these tests.
-    const float so = smag + sqrtf(o2);
+    const float so = smag + pf_sqrt(o2);  // only bounds the magnitudes (1e36 vs fp32's 3.4e38)
     const float so2 = so * so;
     const bool safe = a >= 9.094947e-13f && a <= 1.0995116e12f && n2 >= a * 9.094947e-13f &&
                       so2 <= 1e36f && a * so2 <= 1e36f;
@@ -85,11 +105,19 @@ RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy
         T.thr = -INFINITY;
         return T;
     }
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTX_IEEE_BASIS)  // A/B only: the IEEE basis
     const float sn = sqrtf(n2);
     const float inv_n = 1.0f / sn;
+    const float w = 1.0f / (sqrtf(a) * sn);
+#elif defined(__HIP_DEVICE_COMPILE__)
+    const float inv_n = pf_rsq(n2);  // n2 >= 2^-80 and a >= 2^-40 here: normal inputs
+    const float w = pf_rsq(a) * inv_n;
+#else
+    const float inv_n = pf_rsq_k(n2, 0);
+    const float w = pf_rsq_k(a, 1) * inv_n;
+#endif
     T.ux = -dz * inv_n;
     T.uz = dx * inv_n;
-    const float w = 1.0f / (sqrtf(a) * sn);
     T.vx = (dx * dy) * w;
     T.vy = -(n2 * w);
     T.vz = (dy * dz) * w;

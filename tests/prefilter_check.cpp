@@ -6,7 +6,8 @@
 // whenever the reference's fp32 discriminant is >= 0 or NaN
 // (ShaderCompute.hlsl:158-166; the op order of oracle/rtx_oracle.c
 // hit_world32), the prefilter must flag the sphere — in both op orders the
-// scan uses (line_test_q, and line_test_q_flat for flat blocks).
+// scan uses (line_test_q, and line_test_q_flat for flat blocks), with the
+// line basis's hardware rsq/sqrt modelled as exact or one ulp off either way.
 // Prints one JSON line; exit status 1 if any reference candidate is missed.
 // Build: g++ -O2 -std=c++17 -ffp-contract=off -mfma prefilter_check.cpp
 #include <cmath>
@@ -90,6 +91,8 @@ int main(int argc, char **argv) {
         const double sm = std::sqrt((double)c[0] * c[0] + (double)c[1] * c[1] + (double)c[2] * c[2]) + rf;
         float smag = (float)sm;
         if ((double)smag < sm) smag = std::nextafter(smag, INFINITY);
+        // the basis's 1-ulp hardware rsq/sqrt: exact, or one ulp either way
+        for (int j = 0; j < 3; ++j) rtx::pf_host_ulp[j] = (int)(uni() * 3.0) - 1;
         const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
         const float R = rtx::prefilter_R(c[0], c[1], c[2], r2);
         const float q = rtx::line_test_q(T, c[0], c[1], c[2], R);
