@@ -32,11 +32,27 @@ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y -
 __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+// sqrtf, correctly rounded, with the compiler's own correction of the 1-ulp
+// v_sqrt_f32 (s +- 1 ulp by the sign of the fma residuals) but without its
+// rescaling and class fix-ups where they change nothing: those matter only
+// for 0 < x < 2^-96 (the residuals would be denormal), which takes sqrtf.
+// x = +-0, +inf, NaN and x < 0 come out of the fast sequence as sqrtf gives
+// them (the residuals are NaN or -0 and select nothing).
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    r = fmaf(-sp, s, x) > 0.0f ? sp : r;
+    if (__builtin_expect(x > 0.0f && x < 0x1p-96f, 0)) r = sqrtf(x);
+    return r;
+}
+
 // dot = (x*x' + y*y') + z*z', three roundings of products, two of sums.
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 // normalize(v) = v * (1 / sqrt(dot(v, v)))   (HLSL normalize = v * rsqrt)
 __device__ __forceinline__ f3 normalize3(f3 v) {
-    const float inv = 1.0f / sqrtf(dot3(v, v));
+    const float inv = 1.0f / sqrt_rn(dot3(v, v));
     return inv * v;
 }
 
@@ -161,7 +177,7 @@ __device__ __forceinline__ f3 random_in_unit_sphere(float &seed) {
     const float hx = h.x * 2.0f - 1.0f;
     const float phi = h.y * 6.28318530718f;
     const float r = pow_rt(h.z, 0.333333333f);
-    const float sq = sqrtf(1.0f - hx * hx);
+    const float sq = sqrt_rn(1.0f - hx * hx);
     float sn, cs;
     sincos_rt(phi, sn, cs);
     return f3{r * (sq * sn), r * (sq * cs), r * hx};
@@ -173,7 +189,7 @@ __device__ __forceinline__ f3 random_in_unit_disk(float &seed) {
     float h0, h1;
     hash2(seed, h0, h1);
     const float phi = h1 * 6.28318530718f;
-    const float r = sqrtf(h0 * 1.0f);
+    const float r = sqrt_rn(h0 * 1.0f);
     float sn, cs;
     sincos_rt(phi, sn, cs);
     return f3{r * sn, r * cs, 0.0f};
@@ -187,8 +203,8 @@ __device__ __forceinline__ f3 reflect3(f3 v, f3 n) {
 __device__ __forceinline__ f3 refract3(f3 uv, f3 n, float ratio) {
     const float cos_theta = fminf(dot3(-uv, n), 1.0f);
     const f3 r_perp = ratio * (uv + cos_theta * n);
-    const float lp = sqrtf(dot3(r_perp, r_perp));
-    const float k = -sqrtf(fabsf(1.0f - lp * lp));
+    const float lp = sqrt_rn(dot3(r_perp, r_perp));
+    const float k = -sqrt_rn(fabsf(1.0f - lp * lp));
     return r_perp + k * n;
 }
 // reflectance (:90-97); pow(1-cos, 5) as x^2 * x^2 * x.

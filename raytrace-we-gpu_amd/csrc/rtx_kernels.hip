@@ -148,7 +148,7 @@ __device__ __forceinline__ void diag_add(int k, uint32_t v) {
 // lets a later sphere win an exact tie.
 __device__ __forceinline__ void sphere_roots(float hb, float disc, float inv_a, float t_min,
                                              float &best, int &idx, int i) {
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_rn(disc);
     float root = (-hb - sq) * inv_a;
     bool ok = !(root < t_min || best < root);
     if (!ok) {
@@ -353,9 +353,23 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
 // disc < 0) is skipped, like the reference's `if (d < 0) return false`.
 // Returns false if a candidate has a non-finite root (the lane then takes
 // hit_blocks_seq).
+// The running closest hit of a resolve as one 64-bit key: the root's bits
+// (c >= t_min > 0, or t_max = +inf: bits order like values) above
+// ~(index + 1), so the smaller key is the smaller root, then the larger
+// index among equal roots — the in-order scan's rule (`t_max < root`
+// rejects, :171) as a single unsigned compare. No hit: index -1 (low word ~0).
+__device__ __forceinline__ uint64_t hit_key(float best, int idx) {
+    return ((uint64_t)__float_as_uint(best) << 32) | (uint32_t) ~(uint32_t)(idx + 1);
+}
+__device__ __forceinline__ void key_hit(uint64_t k, float &best, int &idx) {
+    best = __uint_as_float((uint32_t)(k >> 32));
+    idx = (int)~(uint32_t)k - 1;
+}
+
 // One candidate: sc = (center, radius) of sphere g; live = it is one.
+// key: the running closest hit (hit_key).
 __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f3 d, float a, float inv_a,
-                                            float t_min, float &best, int &idx, bool &ok) {
+                                            float t_min, uint64_t &key, bool &ok) {
     const float inf = __uint_as_float(0x7f800000u);
     const float ocx = o.x - sc.x;
     const float ocy = o.y - sc.y;
@@ -363,16 +377,18 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
     const float hb = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));
     const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(sc.w * sc.w))));
     const float disc = fmaf(hb, hb, -(a * cc));
-    const bool cand = live && !(disc < 0.0f);
-    const float sq = sqrtf(disc);
+    const bool cand = live & !(disc < 0.0f);
+    const float sq = sqrt_rn(disc);
     const float rn = (-hb - sq) * inv_a;
     const float rf = (-hb + sq) * inv_a;
-    ok = ok && !(cand && !(fabsf(rn) < inf && fabsf(rf) < inf));
-    const bool use_n = !(rn < t_min);
-    const float c = use_n ? rn : rf;
-    const bool acc = cand && (use_n || !(rf < t_min)) && (c < best || (c == best && g > idx));
-    best = acc ? c : best;
-    idx = acc ? g : idx;
+    ok = ok & !(cand & !(fabsf(rn) < inf & fabsf(rf) < inf));
+    // near root if it is >= t_min, else the far one; accepted if >= t_min
+    // and its key beats the running one (roots finite here: a lane with a
+    // non-finite one is redone by hit_blocks_seq)
+    const float c = !(rn < t_min) ? rn : rf;
+    const uint64_t k = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t) ~(uint32_t)(g + 1);
+    const bool acc = cand & !(c < t_min) & (k < key);
+    key = acc ? k : key;
 }
 
 // `ld(i)` returns (center, radius) of sphere i < n.
@@ -402,17 +418,19 @@ __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t 
     bool l0;
     next(i0, l0);
     float4 v0 = ld(min(i0, n - 1u));
+    uint64_t key = hit_key(best, idx);
     while (__ballot(l0) != 0ull) {
         RTX_DIAG_ADD(2, 1u);
         uint32_t i1;
         bool l1;
         next(i1, l1);
         const float4 v1 = ld(min(i1, n - 1u));
-        resolve_one(v0, (int)i0, l0, o, d, a, inv_a, t_min, best, idx, ok);
+        resolve_one(v0, (int)i0, l0, o, d, a, inv_a, t_min, key, ok);
         i0 = i1;
         l0 = l1;
         v0 = v1;
     }
+    key_hit(key, best, idx);
     return ok;
 }
 __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint32_t n, const uint32_t *list,
@@ -576,8 +594,10 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
                 const uint32_t j = i + u;
                 if (j < i1 && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr)) {
                     const float rr = rad ? rad[j] : S.cen[j].w;
+                    uint64_t key = hit_key(bc, bg);
                     resolve_one(make_float4(pq[u].x, pq[u].y, pq[u].z, rr), (int)j, true, ro, rd, ra, ria, t_min,
-                                bc, bg, ok);
+                                key, ok);
+                    key_hit(key, bc, bg);
                 }
             }
             i = more ? i + kCoopStep : i;
@@ -760,7 +780,7 @@ __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *
         const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(rr * rr))));
         const float disc = fmaf(hb, hb, -(w[6] * cc));
         if (disc < 0.0f) continue;
-        const float sq = sqrtf(disc);
+        const float sq = sqrt_rn(disc);
         const float rn = (-hb - sq) * w[7];
         const float rf = (-hb + sq) * w[7];
         if (!(fabsf(rn) < inf && fabsf(rf) < inf)) {
@@ -919,7 +939,7 @@ __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit,
             const float ratio = ff ? (1.0f / mv.w) : mv.w;
             const f3 ud = normalize3(L.d);
             const float cosine = fminf(dot3(-ud, nrm), 1.0f);
-            const float sine = sqrtf(1.0f - cosine * cosine);
+            const float sine = sqrt_rn(1.0f - cosine * cosine);
             const bool cant = ratio * sine > 1.0f;
             // FXC's `||` does not short-circuit: hash1 always advances the seed.
             const float refl = reflectance(cosine, ratio);
@@ -1671,7 +1691,7 @@ __global__ void __launch_bounds__(kBlock) k_debug_math(int fn, const float *in0,
     const float b = in1 ? in1[i] : 0.0f;
     float seed = a;
     switch (fn) {
-        case 0: out[i] = sqrtf(a); break;
+        case 0: out[i] = sqrt_rn(a); break;
         case 1: out[i] = a / b; break;
         case 2: { float s, c; sincos_rt(a, s, c); out[i] = s; } break;
         case 3: { float s, c; sincos_rt(a, s, c); out[i] = c; } break;

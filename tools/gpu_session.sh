@@ -62,6 +62,11 @@ for s in $STEPS; do
             RTX_LIB=$V run vdiag2 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
                 SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d "$OUT/vdiag2" -o run -- \
                 python3 bench.py --probe ;;
+    vinsts) for v in ${VNAMES:-best}; do  # VALU/SALU instruction counts per variant (deterministic A/B)
+              RTX_LIB=raytrace-we-gpu_amd/lib/variants/librtx_$v.so run vinsts_$v 300 rocprofv3 --pmc SQ_INSTS_VALU \
+                  SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$OUT/vinsts_$v" -o run -- \
+                  python3 bench.py --probe ${VARGS:-}
+              python tools/pmc_sum.py "$OUT/vinsts_$v" "$v" >> "$OUT/vinsts.jsonl"; done ;;
     pmc)    for c in FETCH_SIZE WRITE_SIZE; do
               run pmc_$c 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
                   python3 bench.py --probe ; done ;;
