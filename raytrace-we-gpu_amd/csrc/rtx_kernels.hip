@@ -24,6 +24,8 @@
 // Measured-and-rejected variants (LDS-resident spheres, pre-prefilter scans,
 // ...) are in git history and DESIGN.md §7.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -1373,21 +1375,46 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
 // 2 (slots [k1, kh), kHeavy2 per wave). Tiers and alphas were chosen with
 // tools/part_scaling.py on C2 split 1/2/4/8 ways. Writes kh to heavy[1] and
 // k1 to heavy[3]. One thread: 256 buckets.
-__global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t *heavy) {
+// The split's bars; tools/heavy_sweep.py overrides them
+// through RTX_HEAVY (host side, launch_render) to tune them on the box.
+struct HeavyTune {
+    double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
+};
+static HeavyTune heavy_tune() {
+    HeavyTune t{kHeavy1Alpha, kHeavy1AlphaSmall, kHeavy1AlphaLow, kHeavyAlpha, kHeavy2AlphaMedium,
+                kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0};
+    const char *e = getenv("RTX_HEAVY");  // "a1=1.7,a2s=2,..." (diagnostic tuning only)
+    if (!e) return t;
+    const struct { const char *k; double *v; } keys[] = {
+        {"a1", &t.a1},   {"a1s", &t.a1_small}, {"a1l", &t.a1_low},   {"a2s", &t.a2_small}, {"a2m", &t.a2_medium},
+        {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac}};
+    for (const char *q = e; *q;) {
+        const char *eq = strchr(q, '=');
+        if (!eq) break;
+        for (const auto &k : keys)
+            if (strlen(k.k) == (size_t)(eq - q) && strncmp(q, k.k, eq - q) == 0) *k.v = atof(eq + 1);
+        const char *c = strchr(eq, ',');
+        if (!c) break;
+        q = c + 1;
+    }
+    return t;
+}
+__global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t *heavy,
+                              const HeavyTune t) {
     if (threadIdx.x != 0u) return;
     double w = 0.0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) w += (double)counts[b] * (double)(kCostBuckets - 1u - b);
     const double share = w / (double)(lanes ? lanes : 1u);
-    const bool small = (double)npix < kHeavyRho * (double)lanes;
-    // fewer than kHeavyRhoLow pixels per lane (a 4-way split of C2): tier 1
-    // only above kHeavy1AlphaLow x share — one-ray waves are expensive, and
+    const bool small = (double)npix < t.rho * (double)lanes;
+    // fewer than rho_low pixels per lane (a 4-way split of C2): tier 1
+    // only above a1_low x share — one-ray waves are expensive, and
     // at this share there are many candidates that crowd the SIMDs
-    const bool low = !small && (double)npix < kHeavyRhoLow * (double)lanes;
-    const double a1 = small ? kHeavy1AlphaSmall : low ? kHeavy1AlphaLow : kHeavy1Alpha;
-    // a medium share (fewer than kHeavyRho2 pixels per lane, e.g. a
-    // 2- or 4-way split) also gets tier 2 above kHeavy2AlphaMedium x share
-    const bool medium = !small && (double)npix < kHeavyRho2 * (double)lanes;
-    const double a2 = small ? kHeavyAlpha : medium ? min(kHeavy2AlphaMedium, a1) : a1;
+    const bool low = !small && (double)npix < t.rho_low * (double)lanes;
+    const double a1 = small ? t.a1_small : low ? t.a1_low : t.a1;
+    // a medium share (fewer than rho2 pixels per lane, e.g. a
+    // 2- or 4-way split) also gets tier 2 above a2_medium x share
+    const bool medium = !small && (double)npix < t.rho2 * (double)lanes;
+    const double a2 = small ? t.a2_small : medium ? min(t.a2_medium, a1) : a1;
     uint32_t kh = 0, k1 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
@@ -1888,14 +1915,16 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
     // the persistent render over it
     const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
-    hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy);
+    const HeavyTune tune = heavy_tune();
+    hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy,
+                       tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                        p.rows_local, c.spp, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
     KParams q = p;
     q.cost_spp = c.spp;
     q.perm = sched.perm;
     q.state = sched.state;
-    q.prio_slots = (uint32_t)((uint64_t)blocks * kRB * kPrioFracX100 / 100u);
+    q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;

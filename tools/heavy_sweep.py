@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Sweep the heavy-pixel split's bars (RTX_HEAVY, rtx_kernels.hip
+heavy_tune) on one device: for each setting, the critical part time of an
+R-way row split of C2 (as tools/part_scaling.py). Diagnostic tuning only.
+
+    python tools/heavy_sweep.py --parts 8 --set "a1s=4,a2s=2" --set "a1s=3,a2s=1" ...
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytrace-we-gpu_amd"))
+import rtx  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--parts", type=int, nargs="*", default=[8])
+ap.add_argument("--frames", type=int, default=2)
+ap.add_argument("--rounds", type=int, default=2)
+ap.add_argument("--set", action="append", default=[])
+a = ap.parse_args()
+
+W, H, T = 1920, 1080, 5
+world = rtx.random_world(11, depth=50, spp=100)
+frame = rtx.camera_look_at(W, H, aspect=W / H)
+ctx = rtx.Context(0)
+ctx.upload_world(world)
+ctx.set_frame(frame)
+buf = ctx.alloc((H, W, 4))
+sets = a.set or [""]
+for r in range(a.rounds):
+    for s in sets:
+        if s:
+            os.environ["RTX_HEAVY"] = s
+        else:
+            os.environ.pop("RTX_HEAVY", None)
+        for R in a.parts:
+            times = []
+            for p in range(R):
+                ctx.render_rows(T, p, R, buf.ptr)
+                ctx.sync()
+                ctx.stats_reset()
+                for _ in range(a.frames):
+                    ctx.render_rows(T, p, R, buf.ptr)
+                st = ctx.stats()
+                times.append(st.kernel_ms / st.launches)
+            print(json.dumps({"set": s or "default", "round": r, "parts": R, "critical_ms": round(max(times), 3),
+                              "mean_ms": round(sum(times) / R, 3), "part_ms": [round(t, 3) for t in times]}),
+                  flush=True)
+buf.free()
+ctx.close()
