@@ -65,6 +65,7 @@ struct KParams {
     float4 *state;                 // per pixel (acc, seed) after cost_spp samples: written by the
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
+    uint32_t coop_max;             // queue exhausted: a wave with <= this many pixels traces them in group coop
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels

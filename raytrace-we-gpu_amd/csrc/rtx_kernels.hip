@@ -383,7 +383,8 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
     const float sq = sqrt_rn(disc);
     const float rn = (-hb - sq) * inv_a;
     const float rf = (-hb + sq) * inv_a;
-    ok = ok & !(cand & !(fabsf(rn) < inf & fabsf(rf) < inf));
+    const bool fin = (fabsf(rn) < inf) & (fabsf(rf) < inf);
+    ok = ok & (!cand | fin);
     // near root if it is >= t_min, else the far one; accepted if >= t_min
     // and its key beats the running one (roots finite here: a lane with a
     // non-finite one is redone by hit_blocks_seq)
@@ -682,21 +683,27 @@ __device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float
 }
 
 
-// Sphere-major group coop for 2..kSmRays rays (tier 2 and the frame tail).
+// Sphere-major group coop for kCoopSm..64 rays (tier 2 and the frame tail).
 // The per-ray groups above give each lane one ray and a long run of spheres
 // (61 for 8 rays at C2), tested two at a time: latency-bound. Here lane l
-// tests spheres l, l+64, ... against every ray in turn (the rays' lines
-// are read from LDS once per ray), appends each flagged (sphere, ray) pair
-// to a wave list, and the wave then resolves the list, pairs spread over
-// all lanes, with the reference's ops (the body of resolve_one); every
-// accepted root is folded into its ray's key with an LDS atomic min on
-// (c bits << 32 | ~index), the (min c, largest index) rule of the in-order
-// scan. A non-finite root, or a list overflow (more than kSmCand pairs: an
-// unsafe line flags every sphere), sends the ray (the wave's rays) to the
-// exact sequential path. LDS per wave (coop_ws, 1280 B): rays [8][8] floats,
-// lines [8][8], keys [8] u64, bad [8], count, pairs [kSmCand].
+// tests spheres l, l+64, ... against every ray in turn, two rays per packed
+// instruction (the pair's lines in SGPRs, the sphere broadcast in both
+// halves: 3.5 v_pk_fma_f32 per test, the sphere read from LDS once per pair),
+// appends each flagged (sphere, ray) pair to a wave list, and the wave then
+// resolves the list, pairs spread over all lanes, with the reference's ops
+// (the body of resolve_one); every accepted root is folded into its ray's
+// key with an LDS atomic min on (c bits << 32 | ~index), the (min c,
+// largest index) rule of the in-order scan. The rays go in chunks of
+// kSmRays (ranks [8c, 8c + 8)), one scan + resolve per chunk: a wave of
+// m rays costs ~m/64 of a lane-mode segment in its scan, so a sparse wave
+// (few pixels left, queue empty) runs its segments faster and leaves the
+// SIMD to the others. A non-finite root, or a list overflow (more than
+// kSmCand pairs in a chunk: an unsafe line flags every sphere), sends the
+// ray (the chunk's rays) to the exact sequential path. LDS per wave
+// (coop_ws, 1280 B): rays [8][8] floats, lines [8][8], keys [8] u64,
+// bad [8], count, pairs [kSmCand].
 constexpr int kCoopSm = 4;  // multi-ray coop waves with at least this many rays use groups_sm
-#ifndef RTX_SM_CAND  // sphere-major coop: (sphere, ray) pairs per wave before the exact fallback
+#ifndef RTX_SM_CAND  // sphere-major coop: (sphere, ray) pairs per chunk before the exact fallback
 #define RTX_SM_CAND 160
 #endif
 constexpr uint32_t kSmRays = 8, kSmCand = RTX_SM_CAND;
@@ -706,8 +713,8 @@ __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *
                                          f3 o, f3 d, float a, float inv_a, float t_min, float *ws, float &best,
                                          bool &seq, unsigned long long *cp, unsigned long long *tq) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t m = (uint32_t)__popcll(act);
-    const uint32_t rank =
+    const uint32_t m_all = (uint32_t)__popcll(act);
+    const uint32_t rank_all =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     float *rays = ws;        // [kSmRays][8]: o, d, a, inv_a
     float *lines = ws + 64;  // [kSmRays][8]: LineTest
@@ -715,99 +722,117 @@ __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *
     uint32_t *bad = reinterpret_cast<uint32_t *>(ws + 144);
     uint32_t *count = reinterpret_cast<uint32_t *>(ws + 152);
     uint32_t *pairs = reinterpret_cast<uint32_t *>(ws + 160);
-    if (active) {
-        float *w = rays + 8 * rank;
-        w[0] = o.x;
-        w[1] = o.y;
-        w[2] = o.z;
-        w[3] = d.x;
-        w[4] = d.y;
-        w[5] = d.z;
-        w[6] = a;
-        w[7] = inv_a;
-        const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
-        float *t = lines + 8 * rank;
-        t[0] = T.ux;
-        t[1] = T.uz;
-        t[2] = T.vx;
-        t[3] = T.vy;
-        t[4] = T.vz;
-        t[5] = T.nou;
-        t[6] = T.nov;
-        t[7] = T.thr;
-        keys[rank] = ~0ull;
-        bad[rank] = 0u;
-    }
-    if (lane == 0u) *count = 0u;
-    __builtin_amdgcn_wave_barrier();
-    RTX_CP(0)
+    const LineTest T0 = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const uint32_t n = S.n;
+    const float inf = __uint_as_float(0x7f800000u);
+    int result = -1;
+    seq = false;
 #pragma unroll 1
-    for (uint32_t r = 0; r < m; ++r) {
-        const float *t = lines + 8 * r;  // wave-uniform: kept in scalars
-        LineTest T;
-        T.ux = read_lane(t[0], 0);
-        T.uz = read_lane(t[1], 0);
-        T.vx = read_lane(t[2], 0);
-        T.vy = read_lane(t[3], 0);
-        T.vz = read_lane(t[4], 0);
-        T.nou = read_lane(t[5], 0);
-        T.nov = read_lane(t[6], 0);
-        T.thr = read_lane(t[7], 0);
+    for (uint32_t c0 = 0; c0 < m_all; c0 += kSmRays) {
+        const uint32_t m = min(m_all - c0, kSmRays);
+        const bool mine = active && rank_all >= c0 && rank_all < c0 + m;
+        const uint32_t rank = rank_all - c0;
+        if (mine) {
+            float *w = rays + 8 * rank;
+            w[0] = o.x;
+            w[1] = o.y;
+            w[2] = o.z;
+            w[3] = d.x;
+            w[4] = d.y;
+            w[5] = d.z;
+            w[6] = a;
+            w[7] = inv_a;
+            float *t = lines + 8 * rank;
+            t[0] = T0.ux;
+            t[1] = T0.uz;
+            t[2] = T0.vx;
+            t[3] = T0.vy;
+            t[4] = T0.vz;
+            t[5] = T0.nou;
+            t[6] = T0.nov;
+            t[7] = T0.thr;
+            keys[rank] = ~0ull;
+            bad[rank] = 0u;
+        }
+        if (lane == 0u) *count = 0u;
+        __builtin_amdgcn_wave_barrier();
+        RTX_CP(0)
+#pragma unroll 1
+        for (uint32_t r = 0; r < m; r += 2u) {
+            // rays r and r + 1 (r again when m is odd), wave-uniform: in scalars
+            const uint32_t r1 = min(r + 1u, m - 1u);
+            const float *t0 = lines + 8 * r, *t1 = lines + 8 * r1;
+            auto rl2 = [&](int k) {
+                const f2v v = {read_lane(t0[k], 0), read_lane(t1[k], 0)};
+                return v;
+            };
+            const f2v ux = rl2(0), uz = rl2(1), vx = rl2(2), vy = rl2(3), vz = rl2(4), nou = rl2(5), nov = rl2(6);
+            const float thr0 = read_lane(t0[7], 0), thr1 = read_lane(t1[7], 0);
 #pragma unroll 2
-        for (uint32_t j = lane; j < n; j += 64u) {
-            const float4 pq = sph4[j];
-            if (!(line_test_q(T, pq.x, pq.y, pq.z, pq.w) < T.thr)) {
-                const uint32_t k = atomicAdd(count, 1u);
-                if (k < kSmCand) pairs[k] = (j << 3) | r;
+            for (uint32_t j = lane; j < n; j += 64u) {
+                const float4 pq = sph4[j];
+                const f2v cx = {pq.x, pq.x}, cy = {pq.y, pq.y}, cz = {pq.z, pq.z}, R = {pq.w, pq.w};
+                // line_test_q's ops, per element
+                const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
+                const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
+                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R));
+                if (!(q.x < thr0)) {
+                    const uint32_t k = atomicAdd(count, 1u);
+                    if (k < kSmCand) pairs[k] = (j << 3) | r;
+                }
+                if (r1 != r && !(q.y < thr1)) {
+                    const uint32_t k = atomicAdd(count, 1u);
+                    if (k < kSmCand) pairs[k] = (j << 3) | r1;
+                }
             }
         }
-    }
-    __builtin_amdgcn_wave_barrier();
-    RTX_CP(1)
-    const uint32_t K = *count;
-    const float inf = __uint_as_float(0x7f800000u);
+        __builtin_amdgcn_wave_barrier();
+        RTX_CP(1)
+        const uint32_t K = *count;
 #pragma unroll 1
-    for (uint32_t k = lane; k < min(K, kSmCand); k += 64u) {
-        const uint32_t e = pairs[k];
-        const uint32_t j = e >> 3, r = e & 7u;
-        const float *w = rays + 8 * r;
-        const float4 pq = sph4[j];
-        const float rr = rad ? rad[j] : S.cen[j].w;
-        // resolve_one's ops for one candidate
-        const float ocx = w[0] - pq.x;
-        const float ocy = w[1] - pq.y;
-        const float ocz = w[2] - pq.z;
-        const float hb = fmaf(ocz, w[5], fmaf(ocy, w[4], ocx * w[3]));
-        const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(rr * rr))));
-        const float disc = fmaf(hb, hb, -(w[6] * cc));
-        if (disc < 0.0f) continue;
-        const float sq = sqrt_rn(disc);
-        const float rn = (-hb - sq) * w[7];
-        const float rf = (-hb + sq) * w[7];
-        if (!(fabsf(rn) < inf && fabsf(rf) < inf)) {
-            atomicOr(&bad[r], 1u);
-            continue;
+        for (uint32_t k = lane; k < min(K, kSmCand); k += 64u) {
+            const uint32_t e = pairs[k];
+            const uint32_t j = e >> 3, r = e & 7u;
+            const float *w = rays + 8 * r;
+            const float4 pq = sph4[j];
+            const float rr = rad ? rad[j] : S.cen[j].w;
+            // resolve_one's ops for one candidate
+            const float ocx = w[0] - pq.x;
+            const float ocy = w[1] - pq.y;
+            const float ocz = w[2] - pq.z;
+            const float hb = fmaf(ocz, w[5], fmaf(ocy, w[4], ocx * w[3]));
+            const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(rr * rr))));
+            const float disc = fmaf(hb, hb, -(w[6] * cc));
+            if (disc < 0.0f) continue;
+            const float sq = sqrt_rn(disc);
+            const float rn = (-hb - sq) * w[7];
+            const float rf = (-hb + sq) * w[7];
+            if (!(fabsf(rn) < inf && fabsf(rf) < inf)) {
+                atomicOr(&bad[r], 1u);
+                continue;
+            }
+            const bool use_n = !(rn < t_min);
+            const float c = use_n ? rn : rf;
+            if (use_n || !(rf < t_min))  // c >= t_min > 0: its bits order like its value
+                atomicMin(&keys[r], ((unsigned long long)__float_as_uint(c) << 32) | (unsigned long long)(0xffffffffu - j));
         }
-        const bool use_n = !(rn < t_min);
-        const float c = use_n ? rn : rf;
-        if (use_n || !(rf < t_min))  // c >= t_min > 0: its bits order like its value
-            atomicMin(&keys[r], ((unsigned long long)__float_as_uint(c) << 32) | (unsigned long long)(0xffffffffu - j));
+        __builtin_amdgcn_wave_barrier();
+        RTX_CP(2)
+        if (mine) {
+            if (K > kSmCand || bad[rank] != 0u) {
+                seq = true;
+            } else {
+                const unsigned long long kk = keys[rank];
+                const float c = __uint_as_float((uint32_t)(kk >> 32));
+                if (kk != ~0ull && c <= best) {  // accepted iff c <= t_max
+                    best = c;
+                    result = (int)(0xffffffffu - (uint32_t)kk);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the next chunk reuses the LDS
     }
-    __builtin_amdgcn_wave_barrier();
-    RTX_CP(2)
-    seq = false;
-    if (!active) return -1;
-    if (K > kSmCand || bad[rank] != 0u) {
-        seq = true;
-        return -1;
-    }
-    const unsigned long long kk = keys[rank];
-    if (kk == ~0ull) return -1;
-    const float c = __uint_as_float((uint32_t)(kk >> 32));
-    if (!(c <= best)) return -1;  // accepted iff c <= t_max
-    best = c;
-    return (int)(0xffffffffu - (uint32_t)kk);
+    return active ? result : -1;
 }
 
 #undef RTX_CP
@@ -819,7 +844,6 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, const 
                                                 unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
     if (__popcll(act) == 1)
         return groups_impl<true>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
-    static_assert(kCoopMax <= (int)kSmRays && kHeavy2 <= kSmRays, "coop waves hold <= 8 rays");
     // 2-3 rays: groups of 32 or 16 lanes scan short chunks; from 4 rays on
     // (chunks of 31+ spheres per lane) the sphere-major pass is faster
     if (__popcll(act) >= kCoopSm)
@@ -1195,7 +1219,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         pr[4]++;
         pr[6] += __popcll(act);
 #endif
-        if (heavy || (exhausted && __popcll(act) <= kCoopMax)) {
+        if (heavy || (exhausted && (uint32_t)__popcll(act) <= P.coop_max)) {
 #if RTX_DIAG_PROF
             pr[5]++;
 #endif
@@ -1379,15 +1403,19 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
 // through RTX_HEAVY (host side, launch_render) to tune them on the box.
 struct HeavyTune {
     double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
+    double occ_small, occ_low;  // fraction of the resident waves launched for a small / low share
+    double coop_max;            // KParams::coop_max
 };
 static HeavyTune heavy_tune() {
     HeavyTune t{kHeavy1Alpha, kHeavy1AlphaSmall, kHeavy1AlphaLow, kHeavyAlpha, kHeavy2AlphaMedium,
-                kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0};
+                kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0,
+                1.0,         1.0,               (double)kCoopMax};
     const char *e = getenv("RTX_HEAVY");  // "a1=1.7,a2s=2,..." (diagnostic tuning only)
     if (!e) return t;
     const struct { const char *k; double *v; } keys[] = {
         {"a1", &t.a1},   {"a1s", &t.a1_small}, {"a1l", &t.a1_low},   {"a2s", &t.a2_small}, {"a2m", &t.a2_medium},
-        {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac}};
+        {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac},
+        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"coop", &t.coop_max}};
     for (const char *q = e; *q;) {
         const char *eq = strchr(q, '=');
         if (!eq) break;
@@ -1861,7 +1889,10 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream) {
+hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
+    const HeavyTune tune = heavy_tune();
+    KParams p = p_in;
+    p.coop_max = (uint32_t)min(max(tune.coop_max, 1.0), 64.0);
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t need = ceil_div(lanes, kRB);
@@ -1913,9 +1944,13 @@ hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t s
                        p.rows_local, c.spp, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
-    const uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
+    uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
+    {
+        const double px_per_lane = (double)lanes / ((double)blocks * kRB);
+        const double occ = px_per_lane < tune.rho ? tune.occ_small : px_per_lane < tune.rho_low ? tune.occ_low : 1.0;
+        blocks = max(1u, (uint32_t)(blocks * occ + 0.5));
+    }
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
-    const HeavyTune tune = heavy_tune();
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy,
                        tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,

@@ -660,6 +660,33 @@ def test_flat_block_runs_bit_exact(request, oracle, rtx, ctx_name, ext):
     assert st.segments == segs
 
 
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+@pytest.mark.parametrize("coop", [24, 64])
+def test_sphere_major_chunks_bit_exact(request, oracle, rtx, monkeypatch, ctx_name, coop):
+    """Queue exhausted: waves with up to `coop` pixels left trace them with
+    the sphere-major group coop in chunks of 8 rays, two rays per packed test
+    (RTX_HEAVY coop=..., read by the host at each launch). An 8-way share of
+    a 320x180 frame (fewer pixels than lanes: every wave starts in the tail)
+    and the whole frame, against the oracle; on the stress build every chunk
+    overflows its pair list and takes the exact sequential path."""
+    ctx = request.getfixturevalue(ctx_name)
+    monkeypatch.setenv("RTX_HEAVY", f"coop={coop}")
+    world = rtx.random_world(11, depth=50, spp=10)
+    W, H, T = 320, 180, 5
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    for nparts, part in ((8, 3), (1, 0)):
+        rows = rtx.part_row_ids(H, T, part, nparts)
+        buf = ctx.alloc((H, W, 4))
+        ctx.render_rows(T, part, nparts, buf.ptr)
+        ctx.sync()
+        got = buf.numpy().reshape(-1)[: len(rows) * W * 4].reshape(len(rows), W, 4)
+        buf.free()
+        want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
+        assert_bits_equal(got, want, f"{ctx_name} coop={coop} part {part} of {nparts}")
+
+
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
     """rtx_accumulate: frame k uses frame_index k; the linear sums add up in
     fp32 frame by frame; the framebuffer is toGamma(sum / (k * spp))."""

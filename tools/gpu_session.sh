@@ -43,6 +43,7 @@ for s in $STEPS; do
               run timeline_$v 300 python tools/wave_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_$v.so; done ;;
     sprof)  run sprof 300 python tools/section_prof.py raytrace-we-gpu_amd/lib/variants/librtx_prof.so ;;
     parts)  run parts 600 python tools/part_scaling.py ${PLIBS:-} ;;
+    hsweep) run hsweep 900 python tools/heavy_sweep.py --parts ${HPARTS:-8} --rounds ${HROUNDS:-2} ${HSETS:-} ;;
     psparts) run psparts 600 python tools/part_scaling.py --rng per-sample ;;
     cprof)  run cprof 300 python tools/coop_prof.py raytrace-we-gpu_amd/lib/variants/librtx_cprof.so ;;
     ptime)  run ptime 600 python tools/pixel_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_${PTLIB:-ptime}.so \
