@@ -383,7 +383,7 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
     const float sq = sqrt_rn(disc);
     const float rn = (-hb - sq) * inv_a;
     const float rf = (-hb + sq) * inv_a;
-    const bool fin = (fabsf(rn) < inf) & (fabsf(rf) < inf);
+    const bool fin = fabsf(rn) < inf && fabsf(rf) < inf;
     ok = ok & (!cand | fin);
     // near root if it is >= t_min, else the far one; accepted if >= t_min
     // and its key beats the running one (roots finite here: a lane with a
