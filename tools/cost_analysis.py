@@ -30,6 +30,7 @@ ap.add_argument("--grid", type=int, default=11)
 ap.add_argument("--lanes", type=int, default=6144 * 64)
 ap.add_argument("--out", default="")
 ap.add_argument("--from-npz", default="", help="analyse a saved cost.npz (no GPU)")
+ap.add_argument("--dump-only", action="store_true", help="save the npz and stop")
 a = ap.parse_args()
 
 if a.from_npz:
@@ -43,8 +44,12 @@ else:
     c.set_frame(frame)
     full = c.debug_pixel_cost(0).astype(np.int64)
     one = c.debug_pixel_cost(1).astype(np.int64)
+    two = c.debug_pixel_cost(2).astype(np.int64)  # the scheduled path's 2-spp pre-pass
 if a.out:
-    np.savez_compressed(a.out, full=full.astype(np.uint32), one=one.astype(np.uint32))
+    np.savez_compressed(a.out, full=full.astype(np.uint32), one=one.astype(np.uint32),
+                        **({} if a.from_npz else {"two": two.astype(np.uint32)}))
+if a.dump_only:
+    sys.exit(0)
 
 
 def smooth(x, r):
