@@ -115,8 +115,6 @@ typedef struct rtx_stats {
     uint64_t samples;         /* pixel-samples traced (pixels * spp)             */
     uint64_t segments;        /* hit_world calls (ray segments)                  */
     uint64_t sphere_tests;    /* segments * sphere count (ray-sphere tests)      */
-    uint64_t spec_segments;   /* segments traced speculatively:  */
-                              /* executed work beyond the frame's own segments   */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -263,8 +261,7 @@ enum {
     RTX_FN_SQRT = 0, RTX_FN_DIV = 1, RTX_FN_SIN = 2, RTX_FN_COS = 3,
     RTX_FN_LOG2 = 4, RTX_FN_EXP2 = 5, RTX_FN_POW = 6, RTX_FN_BASEHASH = 7,
     RTX_FN_HASH1 = 8, RTX_FN_HASH2 = 9, RTX_FN_HASH3 = 10, RTX_FN_RIUS = 11,
-    RTX_FN_LAMBERT_DIR = 12, RTX_FN_LAMBERT_DIR_GUARD = 13,
-    RTX_FN_SEED_STEPS = 14  /* in0 = seed, in1 = n: the seed after n literal `seed += 0.1` (1 float) */
+    RTX_FN_LAMBERT_DIR = 12, RTX_FN_LAMBERT_DIR_GUARD = 13
 };
 RTX_API int rtx_debug_math(rtx_ctx *ctx, int fn, const float *in0,
                            const float *in1, uint32_t n, float *out);

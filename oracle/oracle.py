@@ -17,8 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liboracle.so")
 REF_GOLDEN = os.path.join(HERE, "_ref", "ref_golden")
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
-          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13,
-          seed_steps=14)
+          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13)
 
 
 class or_world(C.Structure):
@@ -151,7 +150,7 @@ def math(fn: str, in0, in1=None):
     out = np.zeros(3 * a.size, np.float32)
     if lib().or_math(FN[fn], _f(a), _f(b) if b is not None else None, a.size, _f(out)) != 0:
         raise RuntimeError("or_math failed")
-    return out.reshape(a.size, 3) if FN["hash1"] <= FN[fn] <= FN["lambert_dir_guard"] else out[:a.size]
+    return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
 
 
 def lambert_dir(p, nrm, rius, guard: bool):

@@ -242,10 +242,6 @@ int or_math(int fn, const float *in0, const float *in1, uint32_t n, float *out) 
             case 9: hash2(&seed, &out[3 * i], &out[3 * i + 1]); out[3 * i + 2] = seed; break;
             case 10: h = hash3(&seed); out[3 * i] = h.x; out[3 * i + 1] = h.y; out[3 * i + 2] = h.z; break;
             case 11: h = rius(&seed); out[3 * i] = h.x; out[3 * i + 1] = h.y; out[3 * i + 2] = h.z; break;
-            case 14: /* the chain seed after n literal `seed += 0.1` (ShaderCompute.hlsl:30-48) */
-                for (uint32_t k = 0; k < (uint32_t)b; ++k) seed = seed + 0.1f;
-                out[i] = seed;
-                break;
             default: return -1;
         }
     }

@@ -90,7 +90,6 @@ struct rtx_ctx {
     // per-sample RNG kernel's per-wave sample-colour scratch
     float *d_ps = nullptr;
     size_t ps_floats = 0;
-    void *d_spec = nullptr;  // speculative chain: results [kSpecItemsMax] float4, then offsets
     EventPair events[kEventRing];   // ring: [ev_head, ev_head + ev_count) outstanding
     size_t ev_head = 0, ev_count = 0;
     double ms_folded = 0.0;         // durations of launches whose pair was recycled
@@ -205,7 +204,6 @@ void rtx_destroy(rtx_ctx *c) {
     (void)hipFree(c->d_wave_times);
     (void)hipFree(c->d_sched);
     (void)hipFree(c->d_ps);
-    (void)hipFree(c->d_spec);
     for (auto &p : c->events) {
         if (p.start) (void)hipEventDestroy(p.start);
         if (p.stop) (void)hipEventDestroy(p.stop);
@@ -370,9 +368,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
 
 // Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + 4], then the
 // per-pixel pre-pass state (float4, 16-byte aligned).
-static size_t sched_state_off(size_t npix) {
-    return (2 * npix + 2 * rtx::kCostBuckets + rtx::kHeavyWords + 3) & ~(size_t)3;
-}
+static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 4 + 3) & ~(size_t)3; }
 
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
@@ -503,14 +499,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         RTX_HIP(hipMalloc(&c->d_ps, ps_need * sizeof(float)));
         c->ps_floats = ps_need;
     }
-    // speculative chain buffers (chain RNG, scheduled launches: rtx::spec_wanted)
-    if (!c->d_spec && rtx::spec_wanted(p)) {
-        RTX_HIP(hipMalloc(&c->d_spec, (size_t)rtx::kSpecItemsMax * sizeof(float4) +
-                                          (rtx::kSpecPixMax + 1) * sizeof(uint32_t)));
-    }
     rtx::KSchedule sched;
-    sched.spec_res = reinterpret_cast<float4 *>(c->d_spec);
-    sched.spec_off = c->d_spec ? reinterpret_cast<uint32_t *>(sched.spec_res + rtx::kSpecItemsMax) : nullptr;
     sched.ps_scratch = c->d_ps;
     sched.ps_floats = c->ps_floats;
     sched.cost = c->d_sched;
@@ -602,7 +591,6 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     out->samples = c->samples;
     out->segments = h[0];
     out->sphere_tests = h[0] * (uint64_t)c->n;
-    out->spec_segments = h[1];
     return RTX_OK;
 }
 
@@ -715,9 +703,9 @@ int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_m
 
 int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint32_t n, float *out) {
     if (!c || (n && (!in0 || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_math: null argument");
-    if (fn < RTX_FN_SQRT || fn > RTX_FN_SEED_STEPS)
+    if (fn < RTX_FN_SQRT || fn > RTX_FN_LAMBERT_DIR_GUARD)
         return fail(RTX_ERR_INVALID, "rtx_debug_math: unknown fn");
-    const bool vec = fn == RTX_FN_LAMBERT_DIR || fn == RTX_FN_LAMBERT_DIR_GUARD;  // in0 = p[3n], in1 = (normal, rius)[6n]
+    const bool vec = fn >= RTX_FN_LAMBERT_DIR;  // in0 = p[3n], in1 = (normal, rius)[6n]
     if (vec && n && !in1) return fail(RTX_ERR_INVALID, "rtx_debug_math: lambert functions need in1");
     if (n == 0) return RTX_OK;
     int rc = set_device(c);
@@ -732,7 +720,7 @@ int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint3
     if (e == hipSuccess && in1) e = hipMemcpyAsync(d1, in1, n1 * sizeof(float), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(dout, 0, outn * sizeof(float), c->stream);
     if (e == hipSuccess) e = rtx::launch_debug_math(fn, d0, d1, n, dout, c->stream);
-    const size_t copy_n = (fn >= RTX_FN_HASH1 && fn <= RTX_FN_LAMBERT_DIR_GUARD) ? outn : (size_t)n;
+    const size_t copy_n = (fn >= RTX_FN_HASH1) ? outn : (size_t)n;
     if (e == hipSuccess) e = hipMemcpyAsync(out, dout, copy_n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d0);

@@ -66,14 +66,7 @@ struct KParams {
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t coop_max;             // queue exhausted: a wave with <= this many pixels traces them in group coop
-    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] ns
-                                   // [5] spec items [6] spec item queue [7] spec-slot counter (NULL = none)
-    // speculative chain: queue slots [0, ns) are traced at every
-    // position of their seed sequence; spec_off[j] = first item of slot j (ns + 1
-    // entries), spec_res[item] = (colour.xyz, hash calls | segments << 16) of
-    // the sample that starts at that position
-    float4 *spec_res;
-    uint32_t *spec_off;
+    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
     float *ps_scratch;
@@ -89,17 +82,12 @@ struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
     float4 *state;      // [npix] (acc.xyz, seed) after the pre-pass's samples
-    uint32_t *buckets;  // [2 * nbuckets + kHeavyWords]: counts, cursors, heavy counters and ends (zeroed per launch)
+    uint32_t *buckets;  // [2 * nbuckets + 4]: counts, cursors, heavy counters and ends (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
     float *ps_scratch;  // k_render_ps scratch (rng_mode 1), ps_floats floats
     size_t ps_floats;
-    float4 *spec_res;   // [kSpecItemsMax] speculative samples (NULL: no speculation)
-    uint32_t *spec_off; // [kSpecPixMax + 1]
 };
-constexpr uint32_t kHeavyWords = 8;            // KParams::heavy
-constexpr uint32_t kSpecPixMax = 8192;         // speculated pixels per launch, at most
-constexpr uint32_t kSpecItemsMax = 1u << 22;   // speculative samples per launch, at most (64 MiB of results)
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
 constexpr uint32_t kCostSppLarge = 1;  // ... for scenes above kScanPfMin spheres (C5: 1,997 vs 2,018 ms)
@@ -107,9 +95,6 @@ constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than i
 constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)
 
 hipError_t launch_render(const KParams &p, const KSchedule &sched, hipStream_t stream);
-// True when a launch with these parameters may speculate (chain RNG, scheduled
-// path, and a frame share for which the speculation bar is finite).
-bool spec_wanted(const KParams &p);
 // Floats of k_render_ps scratch a launch with these parameters needs (0 when
 // it takes another kernel).
 size_t ps_scratch_floats(const KParams &p);

@@ -32,7 +32,6 @@
 #include "rtx_device_math.h"
 #include "rtx_internal.h"
 #include "rtx_prefilter.h"
-#include "rtx_seed.h"
 
 namespace rtx {
 
@@ -101,14 +100,6 @@ constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels tha
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 constexpr double kHeavy2AlphaMedium = 1.5;  // tier 2 for a medium share: key > this * share
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
-// speculative chain: bars by share regime (x a lane's share
-// of the summed keys; 1e30 = off) and the traced-position budget factor
-constexpr double kSpecAlphaNormal = 1e30;
-constexpr double kSpecAlphaMedium = 1e30;
-constexpr double kSpecAlphaLow = 3.5;
-constexpr double kSpecAlphaSmall = 4.0;
-constexpr double kSpecFactor = 1.25;
-constexpr uint32_t kSpecDepthMax = 60000;  // hash calls and segments per sample are packed in 16 bits
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
 #define RTX_WAVES_PER_SIMD 5  // occupancy request for the render kernels: 96 VGPRs (the compiler's own
@@ -1071,47 +1062,6 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
     begin_sample(P, F, L.x, L.y, L);
 }
 
-// Start queue slot `slot` < ns, a speculated pixel: k_spec
-// traced the sample that starts at every position k < spec_off[slot + 1] -
-// spec_off[slot] of its seed sequence (position = hash calls after the
-// pre-pass's samples). Follow the chain: sample j starts where sample j - 1
-// ended, acc += its colour in sample order (the same fp32 adds as shade();
-// a black sample's +0 leaves acc unchanged), and its segments count as the
-// frame's. A chain that runs past the traced positions continues from there
-// as an ordinary pixel (seed = the seed at that position); otherwise the pixel
-// is written and the lane stays idle.
-__device__ __forceinline__ void start_spec(const KParams &P, const Frame &F, uint32_t slot, Lane &L) {
-    const uint32_t gid = P.perm[slot];
-    L.gid = gid;
-    lane_pixel(P, gid, L.x, L.y);
-    L.seg0 = L.segs;
-    L.slot = slot;
-    const float4 st = P.state[gid];
-    f3 acc = mk3(st.x, st.y, st.z);
-    const uint32_t o0 = P.spec_off[slot];
-    const uint32_t npos = P.spec_off[slot + 1] - o0;
-    const float4 *__restrict__ res = P.spec_res + o0;
-    uint32_t j = P.cost_spp, pos = 0;
-    while (j < P.spp && pos < npos) {
-        const float4 v = res[pos];
-        acc = acc + mk3(v.x, v.y, v.z);
-        const uint32_t w = __float_as_uint(v.w);
-        pos += w & 0xffffu;
-        L.segs += w >> 16;
-        ++j;
-    }
-    L.acc = acc;
-    if (j >= P.spp) {
-        write_pixel(P, L);
-        L.active = false;
-        return;
-    }
-    L.sample = j;
-    L.seed = seed_advance(st.w, 2u * pos);
-    L.active = true;
-    begin_sample(P, F, L.x, L.y, L);
-}
-
 // Persistent-lane pixel queue: every idle lane of the wave takes the next
 // slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
 // per refill (ballot + lane rank). Returns true once the queue is
@@ -1149,11 +1099,10 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
 // tries tier 1 first; a tier-2 wave tops itself up from tier 2. Returns the
 // wave's tier (0: not heavy any more).
 struct HeavyState {
-    uint32_t ns, k1, kh;  // spec slots [0, ns), tier 1 [ns, k1), tier 2 [k1, kh)
-    bool ts_done, t1_done, t2_done;
+    uint32_t k1, kh;     // tier ends
+    bool t1_done, t2_done;
     uint32_t tier;       // 1, 2, or 0 (normal wave)
 };
-template <bool kSpec = false>
 __device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint32_t *ctr, uint32_t lo, uint32_t hi,
                                           uint32_t room, uint64_t act, Lane &L, bool &done) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1167,10 +1116,7 @@ __device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint
     const uint32_t take = min(room, hi - h);
     const uint32_t rk = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
     if (!L.active && rk < take) {
-        if constexpr (kSpec)
-            start_spec(P, F, h + rk, L);
-        else
-            start_pixel(P, F, P.perm[h + rk], L);
+        start_pixel(P, F, P.perm[h + rk], L);
 #if RTX_DIAG_PIXEL
         if (P.wave_times && L.gid < P.wave_cap)
             P.wave_times[2 * L.gid] = (__builtin_amdgcn_s_memrealtime() << 2) | (ctr == P.heavy ? 1ull : 2ull);
@@ -1183,14 +1129,7 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
     const uint64_t act = __ballot(L.active);
     const uint32_t have = (uint32_t)__popcll(act);
     if (have == 0u) H.tier = 0;
-    // speculated pixels first, a wave's worth at a time: most resolve
-    // completely (lookups only); a chain that outran its traced positions
-    // continues at tier 1
-    if (have == 0u && !H.ts_done && take_from<true>(P, F, P.heavy + 7, 0, H.ns, 64, act, L, H.ts_done)) {
-        H.tier = __ballot(L.active) != 0ull ? 1u : 0u;
-        return;
-    }
-    if (have == 0u && !H.t1_done && take_from(P, F, P.heavy, H.ns, H.k1, kHeavy1, act, L, H.t1_done)) {
+    if (have == 0u && !H.t1_done && take_from(P, F, P.heavy, 0, H.k1, kHeavy1, act, L, H.t1_done)) {
         H.tier = 1;
         return;
     }
@@ -1239,15 +1178,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     }
     // heavy slots [0, kh) of the queue (k_heavy_split; tier 1 = [0, k1)), normal slots [kh, npix)
     HeavyState H;
-    {
-        const uint32_t kh0 = (kPersist && P.heavy) ? min(P.heavy[1], npix) : 0u;
-        const uint32_t k10 = (kPersist && P.heavy) ? min(P.heavy[3], kh0) : 0u;
-        H.ns = (kPersist && P.heavy && P.spec_res) ? min(P.heavy[4], npix) : 0u;
-        H.k1 = max(k10, H.ns);
-        H.kh = max(kh0, H.ns);
-    }
-    H.ts_done = H.ns == 0u;
-    H.t1_done = H.k1 == H.ns;
+    H.kh = (kPersist && P.heavy) ? min(P.heavy[1], npix) : 0u;
+    H.k1 = (kPersist && P.heavy) ? min(P.heavy[3], H.kh) : 0u;
+    H.t1_done = H.k1 == 0u;
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
@@ -1275,19 +1208,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     bool was_t1 = false;
 #endif
     for (;;) {
-        const bool heavy_done = H.ts_done && H.t1_done && H.t2_done;
-        if (!heavy_done && (H.tier != 0u || __ballot(L.active) == 0ull)) take_heavy(P, F, H, L);
+        if (!(H.t1_done && H.t2_done) && (H.tier != 0u || __ballot(L.active) == 0ull)) take_heavy(P, F, H, L);
         if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
         const bool heavy = H.tier != 0u;
         if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
         const uint64_t act = __ballot(L.active);
         RTX_PROF(0)
-        // spp, depth > 0: idle after both queues => drained (a resolved
-        // speculated pixel leaves its lane idle: go back for the next slots)
-        if (act == 0ull) {
-            if (heavy_done) break;
-            continue;
-        }
+        if (act == 0ull) break;  // spp, depth > 0: idle after both queues => drained
 #if RTX_DIAG_PROF
         pr[4]++;
         pr[6] += __popcll(act);
@@ -1478,25 +1405,17 @@ struct HeavyTune {
     double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
     double occ_small, occ_low;  // fraction of the resident waves launched for a small / low share
     double coop_max;            // KParams::coop_max
-    // speculative chain: pixels with key > as_* x share are
-    // speculated (per share regime: normal, medium, low, small; >= kSpecOff =
-    // never), with spec_factor x the estimated positions traced per pixel
-    double as_normal, as_medium, as_low, as_small, spec_factor;
 };
-constexpr double kSpecOff = 1e30;
 static HeavyTune heavy_tune() {
     HeavyTune t{kHeavy1Alpha, kHeavy1AlphaSmall, kHeavy1AlphaLow, kHeavyAlpha, kHeavy2AlphaMedium,
                 kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0,
-                1.0,         1.0,               (double)kCoopMax,
-                kSpecAlphaNormal, kSpecAlphaMedium, kSpecAlphaLow, kSpecAlphaSmall, kSpecFactor};
+                1.0,         1.0,               (double)kCoopMax};
     const char *e = getenv("RTX_HEAVY");  // "a1=1.7,a2s=2,..." (diagnostic tuning only)
     if (!e) return t;
     const struct { const char *k; double *v; } keys[] = {
         {"a1", &t.a1},   {"a1s", &t.a1_small}, {"a1l", &t.a1_low},   {"a2s", &t.a2_small}, {"a2m", &t.a2_medium},
         {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac},
-        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"coop", &t.coop_max},
-        {"asn", &t.as_normal}, {"asm", &t.as_medium}, {"asl", &t.as_low}, {"ass", &t.as_small},
-        {"sf", &t.spec_factor}};
+        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"coop", &t.coop_max}};
     for (const char *q = e; *q;) {
         const char *eq = strchr(q, '=');
         if (!eq) break;
@@ -1524,233 +1443,14 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     // 2- or 4-way split) also gets tier 2 above a2_medium x share
     const bool medium = !small && (double)npix < t.rho2 * (double)lanes;
     const double a2 = small ? t.a2_small : medium ? min(t.a2_medium, a1) : a1;
-    const double as = small ? t.as_small : low ? t.as_low : medium ? t.as_medium : t.as_normal;
-    uint32_t kh = 0, k1 = 0, ns = 0;
+    uint32_t kh = 0, k1 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
         if (key > a2 * share) kh += counts[b];
         if (key > a1 * share) k1 += counts[b];
-        if (key > as * share) ns += counts[b];
     }
     heavy[1] = kh;
     heavy[3] = k1;
-    heavy[4] = min(ns, kSpecPixMax);  // candidates; k_spec_plan fixes the count
-}
-// The share regime's speculation bar, as k_heavy_split picks it (host side).
-static double spec_alpha(const HeavyTune &t, double px_per_lane) {
-    const bool small = px_per_lane < t.rho;
-    const bool low = !small && px_per_lane < t.rho_low;
-    const bool medium = !small && px_per_lane < t.rho2;
-    return small ? t.as_small : low ? t.as_low : medium ? t.as_medium : t.as_normal;
-}
-
-// ---- speculative chain -------------------------------------
-// A pixel's samples form one chain (the reference's RNG, :295, :304-309):
-// sample j+1 starts where sample j's hash calls left the seed, so a heavy
-// pixel's 100 samples run one after another however many lanes are idle —
-// the critical path of a small frame share. But a sample is a pure function
-// of its pixel and its starting seed, and the seed after k hash calls is
-// s_k = seed_advance(s_0, 2k) (rtx_seed.h). So for the heaviest slots
-// [0, ns) of the queue, k_spec traces the sample that starts at EVERY
-// position k < budget of the pixel's seed sequence, one lane per position
-// (the north star's lane-per-sample shape), and records (colour, hash calls,
-// segments); k_render then follows each chain by lookups (start_spec). The
-// result is the chain's, bit for bit; the cost is ~ (positions per sample)
-// times the pixel's work, spent in throughput mode instead of latency.
-//
-// k_spec_plan: per candidate slot j < heavy[4] (k_heavy_split), the budget of
-// positions = spec_factor x (remaining samples) x (estimated hash calls per
-// sample = segments per sample + 1 (+1 with a lens)), segments per sample
-// estimated as max(own, 3x3 mean) of the pre-pass costs; an exclusive prefix
-// over the slots gives spec_off; the slots that fit kSpecItemsMax items are
-// speculated (heavy[4] = ns, heavy[5] = items). One block.
-constexpr uint32_t kPlanThreads = 1024;
-constexpr uint32_t kPlanPer = kSpecPixMax / kPlanThreads;
-__global__ void __launch_bounds__(kPlanThreads)
-    k_spec_plan(const uint32_t *cost, const uint32_t *perm, uint32_t width, uint32_t rows, uint32_t cost_spp,
-                uint32_t spp, uint32_t lens, float factor, uint32_t *heavy, uint32_t *off) {
-    __shared__ uint32_t part[kPlanThreads];
-    __shared__ uint32_t s_ns;
-    const uint32_t nc = min(heavy[4], kSpecPixMax);
-    const uint32_t tid = threadIdx.x;
-    uint32_t bud[kPlanPer];
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < kPlanPer; ++k) {
-        const uint32_t j = tid * kPlanPer + k;
-        bud[k] = 0;
-        if (j < nc) {
-            const uint32_t g = perm[j];
-            const int x = (int)(g % width), y = (int)(g / width);
-            uint32_t nb = 0;
-            for (int dy = -1; dy <= 1; ++dy) {
-                const int yy = min(max(y + dy, 0), (int)rows - 1);
-                for (int dx = -1; dx <= 1; ++dx) nb += cost[(uint32_t)yy * width + (uint32_t)min(max(x + dx, 0), (int)width - 1)];
-            }
-            const float own = (float)cost[g], mean = (float)nb / 9.0f;
-            const float segs = fmaxf(own, mean) / (float)cost_spp;
-            const float calls = segs + 1.0f + (float)lens;
-            const float b = ceilf(factor * (float)(spp - cost_spp) * calls) + 8.0f;
-            bud[k] = (uint32_t)fminf(b, (float)kSpecItemsMax);
-        }
-        sum += bud[k];
-    }
-    part[tid] = sum;
-    if (tid == 0) s_ns = 0;
-    __syncthreads();
-    for (uint32_t d = 1; d < kPlanThreads; d <<= 1) {  // inclusive scan (sums <= kSpecPixMax * 2^22 < 2^35: see clamp)
-        const uint32_t v = tid >= d ? part[tid - d] : 0u;
-        __syncthreads();
-        part[tid] = min(part[tid] + v, 0x7fffffffu);
-        __syncthreads();
-    }
-    uint32_t base = tid ? part[tid - 1] : 0u;
-    for (uint32_t k = 0; k < kPlanPer; ++k) {
-        const uint32_t j = tid * kPlanPer + k;
-        if (j >= nc) break;
-        off[j] = base;
-        base = min(base + bud[k], 0x7fffffffu);
-        if (base <= kSpecItemsMax) atomicMax(&s_ns, j + 1);
-    }
-    __syncthreads();
-    const uint32_t ns = s_ns;  // budgets are positive: the slots that fit form a prefix
-    base = tid ? part[tid - 1] : 0u;
-    for (uint32_t k = 0; k < kPlanPer; ++k) {
-        const uint32_t j = tid * kPlanPer + k;
-        if (j >= nc) break;
-        base += bud[k];
-        if (j + 1 == ns) {
-            off[ns] = base;
-            heavy[5] = base;
-        }
-    }
-    if (tid == 0) {
-        heavy[4] = ns;
-        if (ns == 0) {
-            off[0] = 0;
-            heavy[5] = 0;
-        }
-    }
-}
-
-// k_spec: persistent lanes over the items of the speculated slots (pixel-
-// major, positions ascending: a wave's lanes trace neighbouring positions of
-// one pixel, whose primary rays are coherent). Item t of slot j (the last j
-// with spec_off[j] <= t) is position k = t - spec_off[j]: seed
-// seed_advance(state.seed, 2k), then one whole sample (path regeneration
-// across items, the group coop for a wave's last few paths), recorded as
-// (colour or +0, hash calls | segments << 16). Its segments are speculation,
-// not the frame's: they go to counters[1] (the frame's own are counted when
-// start_spec follows the chain).
-struct SpecLane {
-    f3 o, d, col;
-    float a, inv_a, seed;
-    uint32_t bounce, segs, seg0, item;
-    bool active;
-};
-__device__ __forceinline__ void spec_start(const KParams &P, const Frame &F, uint32_t ns, uint32_t t, SpecLane &L) {
-    uint32_t lo = 0, hi = ns;  // spec_off[lo] <= t < spec_off[hi]
-    while (hi - lo > 1u) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (P.spec_off[mid] <= t) lo = mid; else hi = mid;
-    }
-    const uint32_t gid = P.perm[lo];
-    uint32_t x, y;
-    lane_pixel(P, gid, x, y);
-    L.seed = seed_advance(P.state[gid].w, 2u * (t - P.spec_off[lo]));
-    f3 o, d;
-    start_sample(F, x, y, L.seed, o, d);
-    L.o = o;
-    L.d = d;
-    L.a = dir_len2(d);
-    L.inv_a = 1.0f / L.a;
-    L.col = mk3(1.0f, 1.0f, 1.0f);
-    L.bounce = 0;
-    L.seg0 = L.segs;
-    L.item = t;
-    L.active = true;
-}
-
-template <bool kPF>
-__global__ void RTX_RENDER_BOUNDS k_spec(const KParams P) {
-    // dynamic LDS as k_render: [candidate list][coop rays][LDS copy of the spheres (n <= kCoopLds)]
-    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
-    const uint32_t ns = P.heavy[4], items = P.heavy[5];
-    if (items == 0u) return;  // grid-uniform
-    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    constexpr uint32_t kLB = list_bytes<kPF>();
-    float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
-    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
-    float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
-    const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
-    if (sph_lds) {
-        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
-            s_pre4[i] = P.scene.pre4[i];
-            s_rad[i] = P.scene.cen[i].w;
-        }
-        __syncthreads();
-    }
-    const int last = (int)P.scene.n - 1;
-    const Frame F = load_frame(P);
-    const uint32_t jit = 2u + (F.lens_r > 0.0f ? 1u : 0u);  // hash calls of start_sample
-    const uint32_t lane = threadIdx.x & 63u;
-    SpecLane L;
-    L.active = false;
-    L.segs = 0;
-    bool exhausted = false;
-    for (;;) {
-        if (!exhausted) {
-            const uint64_t idle = __ballot(!L.active);
-            if (idle != 0ull) {
-                const uint32_t cnt = (uint32_t)__popcll(idle);
-                const int leader = __ffsll((long long)idle) - 1;
-                uint32_t base = 0;
-                if ((int)lane == leader) base = atomicAdd(P.heavy + 6, cnt);
-                base = __shfl(base, leader, 64);
-                if (!L.active) {
-                    const uint32_t t = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                    if (t < items) spec_start(P, F, ns, t, L);
-                }
-                exhausted = base + cnt >= items;
-            }
-        }
-        const uint64_t act = __ballot(L.active);
-        if (act == 0ull) break;
-        float best = __uint_as_float(0x7f800000u);
-        int hit = -1;
-        if (exhausted && (uint32_t)__popcll(act) <= P.coop_max) {  // the wave's last few paths
-            __builtin_amdgcn_s_setprio(kTailPrio);
-            bool seq = false;
-            hit = sph_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, (const float *)s_rad, act, L.active,
-                                             L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list, best, seq)
-                          : hit_world_groups(P.scene, P.scene.pre4, (const float *)nullptr, act, L.active, L.o, L.d,
-                                             L.a, L.inv_a, kTMin, coop_ws, list, best, seq);
-            if (L.active && seq) {  // a non-finite root in the group: the exact path
-                best = __uint_as_float(0x7f800000u);
-                hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
-            }
-        } else if (L.active) {
-            hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene,
-                                                  [s_pre4, s_rad](uint32_t i) {
-                                                      const float4 c = s_pre4[i];
-                                                      return make_float4(c.x, c.y, c.z, s_rad[i]);
-                                                  },
-                                                  L.o, L.d, L.a, L.inv_a, kTMin, best, list)
-                          : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
-        }
-        if (L.active) {
-            L.segs++;
-            f3 c = mk3(0.0f, 0.0f, 0.0f);
-            const int r = path_segment(P, L, min(hit, last), best, c);
-            if (r != kSegContinue) {
-                P.spec_res[L.item] = make_float4(c.x, c.y, c.z, __uint_as_float((jit + L.bounce) | ((L.segs - L.seg0) << 16)));
-                L.active = false;
-            }
-        }
-    }
-    uint32_t segs = L.segs;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
-    if (lane == 0u && segs != 0u) atomicAdd(P.counters + 1, (unsigned long long)segs);
 }
 
 // ---- per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample) --
@@ -2058,7 +1758,6 @@ __global__ void __launch_bounds__(kBlock) k_debug_math(int fn, const float *in0,
         case 9: hash2(seed, out[3 * i], out[3 * i + 1]); out[3 * i + 2] = seed; break;
         case 10: { const f3 h = hash3(seed); out[3 * i] = h.x; out[3 * i + 1] = h.y; out[3 * i + 2] = h.z; } break;
         case 11: { const f3 r = random_in_unit_sphere(seed); out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z; } break;
-        case 14: out[i] = seed_advance(a, (uint32_t)b); break;
         default: out[i] = 0.0f;
     }
 }
@@ -2190,14 +1889,6 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
     return hipGetLastError();
 }
 
-static const void *spec_fn(bool pf) { return pf ? (const void *)k_spec<true> : (const void *)k_spec<false>; }
-
-bool spec_wanted(const KParams &p) {
-    const HeavyTune t = heavy_tune();
-    const bool any = t.as_normal < kSpecOff || t.as_medium < kSpecOff || t.as_low < kSpecOff || t.as_small < kSpecOff;
-    return any && p.rng_mode == 0u && p.spp >= kLptMinSpp && p.depth <= kSpecDepthMax;
-}
-
 hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
     const HeavyTune tune = heavy_tune();
     KParams p = p_in;
@@ -2235,7 +1926,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     c.perm = nullptr;  // index order
     c.heavy = nullptr;
     c.prio_slots = 0;
-    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + kHeavyWords) * sizeof(uint32_t), stream);
+    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
     if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (pf) {
@@ -2254,20 +1945,14 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
     uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
-    double px_per_lane = 0.0;
     {
-        px_per_lane = (double)lanes / ((double)blocks * kRB);
+        const double px_per_lane = (double)lanes / ((double)blocks * kRB);
         const double occ = px_per_lane < tune.rho ? tune.occ_small : px_per_lane < tune.rho_low ? tune.occ_low : 1.0;
         blocks = max(1u, (uint32_t)(blocks * occ + 0.5));
     }
-    // speculative chain for this share? (the same regime k_heavy_split picks)
-    const bool spec = sched.spec_res && sched.spec_off && spec_wanted(p) && spec_alpha(tune, px_per_lane) < kSpecOff &&
-                      c.spp < p.spp;
-    HeavyTune st = tune;
-    if (!spec) st.as_normal = st.as_medium = st.as_low = st.as_small = kSpecOff;
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy,
-                       st);
+                       tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                        p.rows_local, c.spp, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
     KParams q = p;
@@ -2276,21 +1961,6 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
-    if (spec) {
-        // 4. speculated slots: budgets, then every position of their chains
-        q.spec_res = sched.spec_res;
-        q.spec_off = sched.spec_off;
-        hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(kPlanThreads), 0, stream, sched.cost, sched.perm, p.width,
-                           p.rows_local, c.spp, p.spp, p.lens_r > 0.0f ? 1u : 0u, (float)tune.spec_factor, heavy,
-                           sched.spec_off);
-        e = allow_lds(spec_fn(pf), lds);
-        if (e != hipSuccess) return e;
-        const uint32_t sb = resident_blocks(spec_fn(pf), lds);
-        if (pf)
-            hipLaunchKernelGGL(k_spec<true>, dim3(sb), dim3(kRB), lds, stream, q);
-        else
-            hipLaunchKernelGGL(k_spec<false>, dim3(sb), dim3(kRB), lds, stream, q);
-    }
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     launch_k<true, false>(pf, blocks, lds, stream, q);

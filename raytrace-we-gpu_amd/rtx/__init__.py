@@ -29,8 +29,7 @@ RTX_OK = 0
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
-          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13,
-          seed_steps=14)
+          hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13)
 FRAME_LAMBERT_GUARD = 1  # rtx_frame.flags bit (RTX_FRAME_LAMBERT_GUARD)
 
 
@@ -55,7 +54,7 @@ class rtx_frame(C.Structure):
 
 class rtx_stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_uint64), ("samples", C.c_uint64),
-                ("segments", C.c_uint64), ("sphere_tests", C.c_uint64), ("spec_segments", C.c_uint64)]
+                ("segments", C.c_uint64), ("sphere_tests", C.c_uint64)]
 
 
 _lib = None
@@ -367,7 +366,7 @@ class Context:
         _check(self._lib.rtx_debug_math(self._h, FN[fn], _fptr(a),
                                         _fptr(b) if b is not None else None, a.size, _fptr(out)),
                "rtx_debug_math")
-        return out.reshape(a.size, 3) if FN["hash1"] <= FN[fn] <= FN["lambert_dir_guard"] else out[:a.size]
+        return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
 
     def debug_lambert_dir(self, p: np.ndarray, nrm: np.ndarray, rius: np.ndarray, guard: bool) -> np.ndarray:
         """The kernel's diffuse direction, normalize(((p + normal) + rius) - p),

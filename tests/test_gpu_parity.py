@@ -776,88 +776,3 @@ def test_upload_rejects_out_of_range_scene(gpu_ctx, rtx):
     with pytest.raises(rtx.RtxError):
         gpu_ctx.upload_world(bad)
     gpu_ctx.upload_world(w)
-
-
-# ---------------------------------------------------------------------------
-# Speculative chain: seed jump, k_spec + chain lookups
-# ---------------------------------------------------------------------------
-def test_seed_advance_matches_literal_steps(gpu_ctx, oracle):
-    """rtx_seed.h's binade-by-binade jump equals the literal `seed += 0.1`
-    additions (the oracle's loop, ShaderCompute.hlsl:30-48) bit for bit."""
-    rng = np.random.default_rng(17)
-    s0 = np.concatenate([rng.integers(0, 2**32, 3000, dtype=np.uint64).astype(np.float32) / np.float32(2**32),
-                         np.array([0.0, 0.125, 0.25, 0.2499999, 1.0, 1023.99, 2048.0], np.float32)])
-    n = np.concatenate([rng.integers(0, 24000, 3000), np.array([0, 1, 2, 3, 10000, 20000, 777])]).astype(np.float32)
-    assert_bits_equal(gpu_ctx.debug_math("seed_steps", s0, n), oracle.math("seed_steps", s0, n), "seed_advance")
-
-
-@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
-@pytest.mark.parametrize("tune", ["ass=0.5,asl=0.5,asm=0.5,asn=0.5",          # many speculated pixels
-                                  "ass=0.5,asl=0.5,asm=0.5,asn=0.5,sf=0.2",   # budgets run out: chains continue
-                                  "ass=0.5,asl=0.5,asm=0.5,asn=0.5,sf=4"])    # every chain resolves by lookups
-def test_speculative_chain_bit_exact(request, oracle, rtx, monkeypatch, ctx_name, tune):
-    """The heaviest queue slots are traced at every position of their seed
-    sequence (k_spec) and resolved by following the chain (start_spec); a
-    chain that outruns its budget continues from the seed at its last
-    position. Whole frame and an 8-way share (every share regime's bar
-    lowered through RTX_HEAVY): bit-exact vs the oracle, and the frame's
-    segment count is the chain's own (speculative work is counted apart)."""
-    ctx = request.getfixturevalue(ctx_name)
-    monkeypatch.setenv("RTX_HEAVY", tune)
-    world = rtx.random_world(11, depth=50, spp=12)
-    W, H, T = 320, 180, 5
-    frame = rtx.camera_look_at(W, H, aspect=W / H)
-    ctx.upload_world(world)
-    ctx.set_frame(frame)
-    for nparts, part in ((1, 0), (8, 5)):
-        rows = rtx.part_row_ids(H, T, part, nparts)
-        buf = ctx.alloc((H, W, 4))
-        ctx.stats_reset()
-        ctx.render_rows(T, part, nparts, buf.ptr)
-        st = ctx.stats()
-        got = buf.numpy().reshape(-1)[: len(rows) * W * 4].reshape(len(rows), W, 4)
-        buf.free()
-        want, segs = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
-        assert_bits_equal(got, want, f"{ctx_name} {tune} part {part} of {nparts}")
-        assert st.segments == segs
-        assert st.spec_segments > 0, "nothing was speculated"
-
-
-@pytest.mark.parametrize("mode", ["thin_lens", "frame_index", "large_scene"])
-def test_speculative_chain_options(gpu_ctx, oracle, rtx, monkeypatch, mode):
-    """Speculation with a lens (3 hash calls per sample start), a progressive
-    frame index (another seed sequence) and a kPF-scan scene (> 1024
-    spheres: k_spec<true>, 1-spp pre-pass)."""
-    monkeypatch.setenv("RTX_HEAVY", "ass=0.5,asl=0.5,asm=0.5,asn=0.5")
-    world = rtx.random_world(20 if mode == "large_scene" else 11, depth=50, spp=9)
-    frame = rtx.camera_look_at(96, 54, aspect=96 / 54)
-    if mode == "thin_lens":
-        frame = rtx.set_aperture(frame, 0.4)
-    elif mode == "frame_index":
-        frame.frame_index = 5
-    img, st = render_gpu(gpu_ctx, world, frame)
-    want, segs = oracle.render_rows(world, frame, np.arange(54), nthreads=min(16, os.cpu_count() or 1))
-    assert_bits_equal(img, want, f"speculative chain, {mode}")
-    assert st.segments == segs
-    assert st.spec_segments > 0
-
-
-def test_speculative_chain_c2_share(gpu_ctx, oracle, rtx):
-    """The default bars on an 8-way share of C2 (the regime speculation is
-    for): rows bit-exact vs the oracle, speculation active."""
-    W, H, T, R, part = 1920, 1080, 5, 8, 6
-    world = rtx.random_world(11, depth=50, spp=100)
-    frame = rtx.camera_look_at(W, H, aspect=W / H)
-    gpu_ctx.upload_world(world)
-    gpu_ctx.set_frame(frame)
-    ids = rtx.part_row_ids(H, T, part, R)
-    buf = gpu_ctx.alloc((len(ids), W, 4))
-    gpu_ctx.stats_reset()
-    gpu_ctx.render_rows(T, part, R, buf.ptr)
-    st = gpu_ctx.stats()
-    got = buf.numpy()
-    buf.free()
-    pick = np.linspace(0, len(ids) - 1, 6).astype(int)
-    want, _ = oracle.render_rows(world, frame, ids[pick], nthreads=min(16, os.cpu_count() or 1))
-    assert_bits_equal(got[pick], want, "C2 8-way share with speculation")
-    assert st.spec_segments > 0

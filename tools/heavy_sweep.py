@@ -36,7 +36,7 @@ for r in range(a.rounds):
         else:
             os.environ.pop("RTX_HEAVY", None)
         for R in a.parts:
-            times, spec = [], []
+            times = []
             for p in range(R):
                 ctx.render_rows(T, p, R, buf.ptr)
                 ctx.sync()
@@ -45,10 +45,8 @@ for r in range(a.rounds):
                     ctx.render_rows(T, p, R, buf.ptr)
                 st = ctx.stats()
                 times.append(st.kernel_ms / st.launches)
-                spec.append(round(st.spec_segments / max(st.segments, 1), 4))
             print(json.dumps({"set": s or "default", "round": r, "parts": R, "critical_ms": round(max(times), 3),
-                              "mean_ms": round(sum(times) / R, 3), "part_ms": [round(t, 3) for t in times],
-                              "spec_over_frame_segments": spec}),
+                              "mean_ms": round(sum(times) / R, 3), "part_ms": [round(t, 3) for t in times]}),
                   flush=True)
 buf.free()
 ctx.close()
