@@ -19,10 +19,13 @@ ap.add_argument("--parts", type=int, nargs="*", default=[8])
 ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--set", action="append", default=[])
+ap.add_argument("--grid", type=int, default=11, help="random_world grid half extent (159 + --max-spheres 100000: C5)")
+ap.add_argument("--max-spheres", type=int, default=0)
+ap.add_argument("--spp", type=int, default=100)
 a = ap.parse_args()
 
 W, H, T = 1920, 1080, 5
-world = rtx.random_world(11, depth=50, spp=100)
+world = rtx.random_world(a.grid, capacity=a.max_spheres or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
 ctx = rtx.Context(0)
 ctx.upload_world(world)
