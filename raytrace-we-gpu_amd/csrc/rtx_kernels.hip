@@ -939,54 +939,83 @@ __device__ __forceinline__ f3 lambert_guard(f3 v, f3 nrm, bool guard) {
 // gradient (:279-283), the sample's colour. LaneT: any lane state with o, d,
 // a, inv_a, col, seed, bounce (Lane, PsLane).
 enum { kSegContinue = 0, kSegSky = 1, kSegBlack = 2 };
+// A wave's lanes take different branches here (sky, Lambert/metal,
+// dielectric) and every branch with a live lane costs the whole wave, so the
+// operations the branches have in common run once, for all the lanes that
+// need them, each lane still executing exactly the HLSL's op sequence:
+//  * normalize(d): the sky (:281) and the dielectric (:231);
+//  * one hash step: random_in_unit_sphere's hash3 (:60) and the dielectric's
+//    hash1 (:241) each consume exactly one `float2(seed += .1, seed += .1)`
+//    and baseHash of it; the lane then converts the hash as its call would;
+//  * sqrt(1 - x*x): random_in_unit_sphere's sqrt(1 - h.x^2) (:63) and the
+//    dielectric's sin_theta = sqrt(1 - cos_theta^2) (:234).
 template <typename LaneT>
 __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit, float t, f3 &sky_col) {
+    const KScene &S = P.scene;
+    int mt = 3;
+    f3 p = L.o, nrm = L.d;
+    bool ff = false;
+    float4 mv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (hit >= 0) {
-        const KScene &S = P.scene;
         const float4 sc = S.cen[hit];
-        const f3 p = L.o + t * L.d;                    // Ray::at, Ray.h:16-19
+        p = L.o + t * L.d;                             // Ray::at, Ray.h:16-19
         const float inv_r = 1.0f / sc.w;               // Vec3 operator/, Vec3.h:83-86
-        f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));  // Sphere.cpp:28
-        const bool ff = dot3(L.d, nrm) < 0.0f;         // set_face_normal, :143-150
+        nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));     // Sphere.cpp:28
+        ff = dot3(L.d, nrm) < 0.0f;                    // set_face_normal, :143-150
         if (!ff) nrm = -nrm;
-        const int mt = S.mtype[hit];
-        const float4 mv = S.mval[hit];
-        f3 dir;
+        mt = S.mtype[hit];
+        mv = S.mval[hit];
+    }
+    const bool sky = hit < 0;
+    const bool diel = !sky && mt == 2;
+    f3 ud = L.d;
+    if (sky || diel) ud = normalize3(L.d);
+    if (sky) {
+        const float tt = 0.5f * (ud.y + 1.0f);
+        const float w = 1.0f - tt;
+        const f3 sk = mk3(w + tt * 0.5f, w + tt * 0.7f, w + tt);
+        sky_col = L.col * sk;
+        return kSegSky;
+    }
+    if (mt != 0 && mt != 1 && !diel) return kSegBlack;  // unknown material: sample is black (:251, :274)
+    const uint32_t hn = hash_step(L.seed);
+    float x, cosine = 0.0f, ratio = 0.0f, hx = 0.0f, phi = 0.0f, hz = 0.0f;
+    if (diel) {  // DIELECTRIC (:229-249), atten = 1
+        ratio = ff ? (1.0f / mv.w) : mv.w;
+        cosine = fminf(dot3(-ud, nrm), 1.0f);
+        x = cosine;
+    } else {     // random_in_unit_sphere's hash3 (:43-48, :59-66)
+        hx = ((float)(hn & 0x7fffffffu) / 2147483648.0f) * 2.0f - 1.0f;
+        phi = ((float)((hn * 16807u) & 0x7fffffffu) / 2147483648.0f) * 6.28318530718f;
+        hz = (float)((hn * 48271u) & 0x7fffffffu) / 2147483648.0f;
+        x = hx;
+    }
+    const float sq = sqrt_rn(1.0f - x * x);
+    f3 dir;
+    if (diel) {
+        const bool cant = ratio * sq > 1.0f;
+        // FXC's `||` does not short-circuit: hash1 always advances the seed.
+        const float refl = reflectance(cosine, ratio);
+        const float h = (float)hn / 4294967296.0f;  // hash1 (:30-34)
+        dir = (cant || refl > h) ? reflect3(ud, nrm) : refract3(ud, nrm, ratio);
+    } else {
         // Lambert and metal share random_in_unit_sphere and normalize: run
         // them once for both kinds of lane (each lane's ops are the HLSL's).
-        if (mt == 0 || mt == 1) {
-            const f3 rius = random_in_unit_sphere(L.seed);
-            const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
-                                 : reflect3(L.d, nrm) + mv.w * rius;     // METAL (:219-227)
-            dir = normalize3(lambert_guard(v, nrm, mt == 0 && (P.flags & kFrameLambertGuard) != 0u));
-            L.col = L.col * mk3(mv.x, mv.y, mv.z);
-        } else if (mt == 2) {
-            // DIELECTRIC (:229-249), atten = 1
-            const float ratio = ff ? (1.0f / mv.w) : mv.w;
-            const f3 ud = normalize3(L.d);
-            const float cosine = fminf(dot3(-ud, nrm), 1.0f);
-            const float sine = sqrt_rn(1.0f - cosine * cosine);
-            const bool cant = ratio * sine > 1.0f;
-            // FXC's `||` does not short-circuit: hash1 always advances the seed.
-            const float refl = reflectance(cosine, ratio);
-            const float h = hash1(L.seed);
-            dir = (cant || refl > h) ? reflect3(ud, nrm) : refract3(ud, nrm, ratio);
-        } else {
-            return kSegBlack;  // unknown material: sample is black (:251, :274)
-        }
-        L.o = p;
-        L.d = dir;
-        L.a = dir_len2(dir);
-        L.inv_a = 1.0f / L.a;
-        L.bounce++;
-        return L.bounce >= P.depth ? kSegBlack : kSegContinue;  // depth exhausted -> black (:286)
+        const float r = pow_rt(hz, 0.333333333f);
+        float sn, cs;
+        sincos_rt(phi, sn, cs);
+        const f3 rius = f3{r * (sq * sn), r * (sq * cs), r * hx};
+        const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
+                             : reflect3(L.d, nrm) + mv.w * rius;     // METAL (:219-227)
+        dir = normalize3(lambert_guard(v, nrm, mt == 0 && (P.flags & kFrameLambertGuard) != 0u));
+        L.col = L.col * mk3(mv.x, mv.y, mv.z);
     }
-    const f3 ud = normalize3(L.d);
-    const float tt = 0.5f * (ud.y + 1.0f);
-    const float w = 1.0f - tt;
-    const f3 sky = mk3(w + tt * 0.5f, w + tt * 0.7f, w + tt);
-    sky_col = L.col * sky;
-    return kSegSky;
+    L.o = p;
+    L.d = dir;
+    L.a = dir_len2(dir);
+    L.inv_a = 1.0f / L.a;
+    L.bounce++;
+    return L.bounce >= P.depth ? kSegBlack : kSegContinue;  // depth exhausted -> black (:286)
 }
 
 // Chain-RNG lane: one segment, then the pixel's next sample when the path

@@ -22,11 +22,13 @@ ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--tile-rows", type=int, default=5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
+ap.add_argument("--grid", type=int, default=11, help="random_world grid half extent (159 + --max-spheres 100000: C5)")
+ap.add_argument("--max-spheres", type=int, default=0)
 ap.add_argument("libs", nargs="*")
 a = ap.parse_args()
 
 W, H = 1920, 1080
-world = rtx.random_world(11, depth=50, spp=a.spp)
+world = rtx.random_world(a.grid, capacity=a.max_spheres or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
 frame.rng_mode = 1 if a.rng == "per-sample" else 0
 for path in a.libs or [None]:
