@@ -230,6 +230,17 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // loaded registers ("+s") so that nothing reads them before it. Every path
 // out of the loop body passes a wait, so no load is in flight at exit.
 constexpr uint32_t kScanPfMin = 1024;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
+#ifndef RTX_PACK  // kPF scans start where the workgroup's other waves are (hit_world_pre_ld)
+#define RTX_PACK 1
+#endif
+#ifndef RTX_PACK_EVERY
+#define RTX_PACK_EVERY 16
+#endif
+#ifndef RTX_PACK_LAG
+#define RTX_PACK_LAG 8
+#endif
+constexpr uint32_t kPackEvery = RTX_PACK_EVERY;  // blocks between position updates (a power of two)
+constexpr uint32_t kPackLag = RTX_PACK_LAG;      // a new scan starts this many blocks behind the last update
 typedef float f16v __attribute__((ext_vector_type(16)));
 // Issue block p's loads; the "+v" operands (the line's basis, which every
 // VALU instruction of the scan reads) keep the compiler from scheduling the
@@ -248,7 +259,8 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 // stopped because some lane's list is full.
 template <bool kPF, bool kFlat>
 __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_t end, const LineTest &T,
-                                               float kvn1, uint32_t *my, uint32_t &cnt, bool &full) {
+                                               float kvn1, uint32_t *my, uint32_t &cnt, bool &full,
+                                               uint32_t *pack) {
     f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
     f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, kvn = {kvn1, kvn1};
     const f2v th = {T.thr, T.thr};
@@ -306,6 +318,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             sload_wait(b_lo, b_hi);
             if (f) return b + 1;
             if (++b >= end) break;
+            if (RTX_PACK && (b & (kPackEvery - 1u)) == 0u && (threadIdx.x & 63u) == 0u) *pack = b;
             sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
             f = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
             sload_wait(a_lo, a_hi);
@@ -325,21 +338,22 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
 // The scan over blocks [b, nblk): the scene's flat run [flat_lo, flat_hi)
 // (rtx_internal.h KScene) with the 6-op test, the rest with the 7-op one.
 // Returns the block to resume at: nblk, or earlier once some lane's list is
-// full (wave-uniform).
+// full (wave-uniform). kPF scans publish their position to `pack` (below).
 template <bool kPF>
 __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk, const LineTest &T,
-                                                   const KScene &S, uint32_t *list, uint32_t &cnt) {
+                                                   const KScene &S, uint32_t *list, uint32_t &cnt,
+                                                   uint32_t *pack = nullptr) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
     const float kv = line_test_kv(T, S.flat_cy);
     while (b < nblk) {
         bool full;
         if (b < S.flat_lo) {
-            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nov, my, cnt, full);
+            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nov, my, cnt, full, pack);
         } else if (b < S.flat_hi) {
-            b = scan_range<kPF, true>(pre, b, S.flat_hi, T, kv, my, cnt, full);
+            b = scan_range<kPF, true>(pre, b, min(S.flat_hi, nblk), T, kv, my, cnt, full, pack);
         } else {
-            b = scan_range<kPF, false>(pre, b, nblk, T, T.nov, my, cnt, full);
+            b = scan_range<kPF, false>(pre, b, nblk, T, T.nov, my, cnt, full, pack);
         }
         if (full) break;
     }
@@ -449,21 +463,40 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // hit_blocks_seq.
 // `ld(i)` returns (center, radius) of sphere i for the resolve (cen in HBM,
 // or, for scenes up to kCoopLds spheres, the block's LDS copy of them).
+// pack (kPF kernels, RTX_PACK): the workgroup's LDS word holding the block a
+// wave of it scanned last (published every kPackEvery blocks). A segment's
+// scan starts kPackLag blocks behind it and wraps round — [b0, nblk) then
+// [0, b0): the resolution rule is order-independent, so any start gives the
+// in-order answer — so the workgroup's waves stream the 100k-sphere array
+// together and a block one wave brought into the scalar cache serves the
+// waves that trail it, instead of every wave missing on every block.
 template <bool kPF, typename Ld>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
-                                                float t_min, float &best, uint32_t *list) {
+                                                float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr) {
     const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const float best0 = best;
     int idx = -1;
     bool ok = true;
-    uint32_t b = 0;
-    do {
+    uint32_t b0 = 0;
+    if (RTX_PACK && kPF && pack) {
+        const uint32_t at = __builtin_amdgcn_readfirstlane(*pack);  // wave-uniform (SGPR)
+        b0 = at < nblk ? (at + nblk - kPackLag) % nblk : 0u;  // nblk > 128 > kPackLag
+    }
+    uint32_t b = b0, end = nblk;
+    for (;;) {
         uint32_t cnt;
-        b = scan_prefilter<kPF>(pre, b, nblk, T, S, list, cnt);
+        b = scan_prefilter<kPF>(pre, b, end, T, S, list, cnt, pack);
         ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
-    } while (b < nblk);
+        if (b < end) continue;
+        if (end == nblk && b0 != 0u) {  // wrap round to the start
+            b = 0;
+            end = b0;
+            continue;
+        }
+        break;
+    }
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
@@ -473,9 +506,9 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
 }
 template <bool kPF>
 __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
-                                             float t_min, float &best, uint32_t *list) {
+                                             float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr) {
     const float4 *__restrict__ cen = S.cen;
-    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list);
+    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list, pack);
 }
 
 // ---- group-cooperative hit_world (frame tail) ------------------------------
@@ -1185,11 +1218,16 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
     float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
     const bool coop_lds = P.scene.n <= kCoopLds;
+    // kPF scenes never fit the LDS copy: its place holds the scan's pack word
+    uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
     if (coop_lds) {
         for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
             s_pre4[i] = P.scene.pre4[i];
             s_rad[i] = P.scene.cen[i].w;
         }
+        __syncthreads();
+    } else if (kPF) {
+        if (threadIdx.x == 0) *pack = 0u;
         __syncthreads();
     }
     const int last = (int)P.scene.n - 1;
@@ -1318,7 +1356,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                             return make_float4(c.x, c.y, c.z, s_rad[i]);
                                                         },
                                                         L.o, L.d, L.a, L.inv_a, kTMin, best, list)
-                                : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+                                : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             RTX_PROF(1)
             shade<kCost>(P, F, L, min(hit, last), best);
         }
@@ -1850,7 +1888,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes +
+    return (use_pf(s) ? list_bytes<true>() + 16 : kListBytes) + kCoopBytes +  // kPF: the pack word
            (s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
 }
 
