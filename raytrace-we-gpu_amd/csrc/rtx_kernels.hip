@@ -318,6 +318,13 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             sload_wait(b_lo, b_hi);
             if (f) return b + 1;
             if (++b >= end) break;
+            // publish the position at b = 0 mod kPackEvery, from this half of
+            // the ping-pong only: it sees blocks of one parity, so only scans
+            // that started at an odd block publish — in practice the flat run
+            // that resumes at block 1 after the ground sphere's block 0, i.e.
+            // the wrapped leg of a segment. Publishing from both halves (every
+            // scan) measured no faster than no pack at all, this 4-7 % faster
+            // (DESIGN.md §7 R4k-q).
             if (RTX_PACK && (b & (kPackEvery - 1u)) == 0u && (threadIdx.x & 63u) == 0u) *pack = b;
             sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
             f = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
