@@ -1477,19 +1477,19 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
 // through RTX_HEAVY (host side, launch_render) to tune them on the box.
 struct HeavyTune {
     double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
-    double occ_small, occ_low;  // fraction of the resident waves launched for a small / low share
+    double occ_small, occ_low, occ_normal;  // fraction of the resident waves launched for a small / low / larger share
     double coop_max;            // KParams::coop_max
 };
 static HeavyTune heavy_tune() {
     HeavyTune t{kHeavy1Alpha, kHeavy1AlphaSmall, kHeavy1AlphaLow, kHeavyAlpha, kHeavy2AlphaMedium,
                 kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0,
-                1.0,         1.0,               (double)kCoopMax};
+                1.0,         1.0,               1.0,               (double)kCoopMax};
     const char *e = getenv("RTX_HEAVY");  // "a1=1.7,a2s=2,..." (diagnostic tuning only)
     if (!e) return t;
     const struct { const char *k; double *v; } keys[] = {
         {"a1", &t.a1},   {"a1s", &t.a1_small}, {"a1l", &t.a1_low},   {"a2s", &t.a2_small}, {"a2m", &t.a2_medium},
         {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac},
-        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"coop", &t.coop_max}};
+        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"occn", &t.occ_normal}, {"coop", &t.coop_max}};
     for (const char *q = e; *q;) {
         const char *eq = strchr(q, '=');
         if (!eq) break;
@@ -2021,7 +2021,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
     {
         const double px_per_lane = (double)lanes / ((double)blocks * kRB);
-        const double occ = px_per_lane < tune.rho ? tune.occ_small : px_per_lane < tune.rho_low ? tune.occ_low : 1.0;
+        const double occ = px_per_lane < tune.rho ? tune.occ_small : px_per_lane < tune.rho_low ? tune.occ_low : tune.occ_normal;
         blocks = max(1u, (uint32_t)(blocks * occ + 0.5));
     }
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
