@@ -45,13 +45,10 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best nopack merge donate8 donate32 lag0 lag32 every4 noflat ieeebasis prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psnostore psb80 psb20
+VARIANTS := best nopack lag0 lag32 every4 noflat ieeebasis prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psnostore psb80 psb20
 VFLAGS_best          :=
 VFLAGS_noflat        := -DRTX_FLAT=0
 VFLAGS_nopack        := -DRTX_PACK=0
-VFLAGS_merge         := -DRTX_MERGE=1
-VFLAGS_donate8       := -DRTX_MERGE=1 -DRTX_DONATE_MAX=8
-VFLAGS_donate32      := -DRTX_MERGE=1 -DRTX_DONATE_MAX=32
 VFLAGS_lag0          := -DRTX_PACK_LAG=0
 VFLAGS_lag32         := -DRTX_PACK_LAG=32
 VFLAGS_every4        := -DRTX_PACK_EVERY=4

@@ -1207,129 +1207,6 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
         H.tier = 2;
 }
 
-// ---- lane merging inside a workgroup (RTX_MERGE) ---------------------------
-// Once the queue is empty a wave runs until its last pixel ends, and every
-// iteration costs the SIMD a full wave-iteration however few lanes are live:
-// in a small frame share (an 8-way split: fewer pixels than lanes) most of
-// the share is such sparse waves. A sparse wave (<= kDonateMax live lanes)
-// with a denser wave in its workgroup becomes a donor: each lane of it that
-// is at a sample boundary (a fresh primary ray, bounce 0) is moved through
-// an LDS mailbox into an idle lane of a denser wave, which traces it from
-// there — the same state, so the same ops and results — and the donor exits
-// once it is empty. The last live wave of the workgroup takes whatever the
-// mailbox still holds, so no pixel is dropped. LDS: [lock, count, live, -,
-// live lanes of wave 0..3][kMergeCap entries of kMergeWords words].
-#ifndef RTX_MERGE
-#define RTX_MERGE 0
-#endif
-constexpr uint32_t kMergeCap = 32;
-constexpr uint32_t kMergeWords = 16;
-constexpr uint32_t kMergeBytes = 8 * 4 + kMergeCap * kMergeWords * 4;
-#ifndef RTX_DONATE_MAX
-#define RTX_DONATE_MAX 16
-#endif
-constexpr uint32_t kDonateMax = RTX_DONATE_MAX;
-__device__ __forceinline__ void mb_lock(uint32_t *mb) {
-    if ((threadIdx.x & 63u) == 0u)
-        while (atomicCAS(mb, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void mb_unlock(uint32_t *mb) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63u) == 0u) atomicExch(mb, 0u);
-}
-// One merge step of a wave whose queue work is done (queue empty, no heavy
-// slot left, not a heavy wave). `donor`: this wave gives its lanes away.
-__device__ __forceinline__ void merge_step(const KParams &P, uint32_t *mb, bool &donor, Lane &L) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    volatile uint32_t *vh = mb;
-    uint32_t *ent = mb + 8;
-    const uint64_t act = __ballot(L.active);
-    const uint32_t my = (uint32_t)__popcll(act);
-    if (!donor) {
-        if (lane == 0u) vh[4 + w] = my;
-        if (my < 64u && vh[1] != 0u) {  // take waiting lanes into idle ones
-            mb_lock(mb);
-            const uint32_t cnt = vh[1];
-            const uint32_t k = min(64u - my, cnt);
-            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(~act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)~act, 0u));
-            if (!L.active && r < k) {
-                const uint32_t *e = ent + (cnt - 1u - r) * kMergeWords;
-                L.gid = e[0];
-                L.x = e[1];
-                L.y = e[2];
-                L.slot = e[3];
-                L.sample = e[4];
-                L.seed = __uint_as_float(e[5]);
-                L.acc = mk3(__uint_as_float(e[6]), __uint_as_float(e[7]), __uint_as_float(e[8]));
-                L.o = mk3(__uint_as_float(e[9]), __uint_as_float(e[10]), __uint_as_float(e[11]));
-                set_dir(L, mk3(__uint_as_float(e[12]), __uint_as_float(e[13]), __uint_as_float(e[14])));
-                L.col = mk3(1.0f, 1.0f, 1.0f);
-                L.bounce = 0;
-                L.active = true;
-            }
-            if (lane == 0u) vh[1] = cnt - k;
-            mb_unlock(mb);
-            if (lane == 0u) vh[4 + w] = (uint32_t)__popcll(__ballot(L.active));
-            return;
-        }
-        if (my == 0u || my > kDonateMax) return;
-        // a denser live non-donor wave (ties: the lower index receives) with room for us
-        bool dense = false;
-        for (uint32_t v = 0; v < kRB / 64; ++v) {
-            const uint32_t a = vh[4 + v];
-            dense |= v != w && a != 0u && (a > my || (a == my && v < w)) && a + my <= 64u;
-        }
-        if (!dense) return;
-        donor = true;
-        if (lane == 0u) vh[4 + w] = 0u;
-    }
-    const uint64_t fresh = __ballot(L.active && L.bounce == 0u);
-    if (fresh == 0ull) return;
-    mb_lock(mb);
-    const uint32_t cnt = vh[1];
-    const uint32_t k = min((uint32_t)__popcll(fresh), kMergeCap - cnt);
-    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(fresh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fresh, 0u));
-    if (L.active && L.bounce == 0u && r < k) {
-        uint32_t *e = ent + (cnt + r) * kMergeWords;
-        e[0] = L.gid;
-        e[1] = L.x;
-        e[2] = L.y;
-        e[3] = L.slot;
-        e[4] = L.sample;
-        e[5] = __float_as_uint(L.seed);
-        e[6] = __float_as_uint(L.acc.x);
-        e[7] = __float_as_uint(L.acc.y);
-        e[8] = __float_as_uint(L.acc.z);
-        e[9] = __float_as_uint(L.o.x);
-        e[10] = __float_as_uint(L.o.y);
-        e[11] = __float_as_uint(L.o.z);
-        e[12] = __float_as_uint(L.d.x);
-        e[13] = __float_as_uint(L.d.y);
-        e[14] = __float_as_uint(L.d.z);
-        L.active = false;
-    }
-    if (lane == 0u) vh[1] = cnt + k;
-    mb_unlock(mb);
-}
-// A wave with no live lane may exit unless it is the workgroup's last live
-// wave and the mailbox still holds lanes: then it stays (and takes them).
-__device__ __forceinline__ bool merge_may_exit(uint32_t *mb, bool &donor) {
-    volatile uint32_t *vh = mb;
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t old = 0;
-    if (lane == 0u) old = atomicSub(mb + 2, 1u);
-    old = __builtin_amdgcn_readfirstlane(old);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (old == 1u && vh[1] != 0u) {
-        if (lane == 0u) atomicAdd(mb + 2, 1u);
-        donor = false;
-        return false;
-    }
-    if (lane == 0u) vh[4 + w] = 0u;
-    return true;
-}
-
 // Render kernel (chain RNG), per-wave independent; sphere blocks are read
 // with scalar loads (a block-wide LDS copy serves the coop and the resolve of
 // scenes up to kCoopLds spheres). kPersist: the grid holds as many waves as the GPU keeps resident and
@@ -1350,11 +1227,6 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const bool coop_lds = P.scene.n <= kCoopLds;
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
-    // lane merging (persistent render of small scenes): the mailbox after the sphere copy
-    constexpr bool kMerge = RTX_MERGE && kPersist && !kCost && !kPF;
-    uint32_t *mb = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes +
-                                                (coop_lds ? ((P.scene.n * 20u + 15u) & ~15u) : 0u));
-    if (kMerge && threadIdx.x < 8u) mb[threadIdx.x] = threadIdx.x == 2u ? kRB / 64 : 0u;
     if (coop_lds) {
         for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
             s_pre4[i] = P.scene.pre4[i];
@@ -1364,10 +1236,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     } else if (kPF) {
         if (threadIdx.x == 0) *pack = 0u;
         __syncthreads();
-    } else if (kMerge) {
-        __syncthreads();
     }
-    bool donor = false;
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
@@ -1417,13 +1286,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
         const bool heavy = H.tier != 0u;
         if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
-        if (kMerge && exhausted && !heavy && H.t1_done && H.t2_done) merge_step(P, mb, donor, L);
         const uint64_t act = __ballot(L.active);
         RTX_PROF(0)
-        if (act == 0ull) {  // spp, depth > 0: idle after both queues => drained
-            if (kMerge && !merge_may_exit(mb, donor)) continue;
-            break;
-        }
+        if (act == 0ull) break;  // spp, depth > 0: idle after both queues => drained
 #if RTX_DIAG_PROF
         pr[4]++;
         pr[6] += __popcll(act);
@@ -2031,8 +1896,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() + 16 : kListBytes) + kCoopBytes +  // kPF: the pack word
-           (s.n <= kCoopLds ? (((size_t)s.n * (sizeof(float4) + sizeof(float)) + 15) & ~(size_t)15) : 0) +
-           (RTX_MERGE && !use_pf(s) ? kMergeBytes : 0);  // the merge mailbox (k_render<true> only uses it)
+           (s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
