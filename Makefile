@@ -45,14 +45,13 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best nopack lag0 lag32 every4 noflat ieeebasis prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psnostore psb80 psb20
+VARIANTS := best nopack lag0 lag32 every4 noflat prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psb80 psb20
 VFLAGS_best          :=
 VFLAGS_noflat        := -DRTX_FLAT=0
 VFLAGS_nopack        := -DRTX_PACK=0
 VFLAGS_lag0          := -DRTX_PACK_LAG=0
 VFLAGS_lag32         := -DRTX_PACK_LAG=32
 VFLAGS_every4        := -DRTX_PACK_EVERY=4
-VFLAGS_ieeebasis     := -DRTX_IEEE_BASIS=1
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
@@ -61,11 +60,10 @@ VFLAGS_cprof2        := -DRTX_DIAG_COOP=2
 VFLAGS_cand24        := -DRTX_CAND=24
 VFLAGS_cand6         := -DRTX_CAND=6
 VFLAGS_pfcand12      := -DRTX_CAND_PF=12
-# per-sample kernel: items per batch slot; timing diagnostic without the colour stores
+# per-sample kernel: items per batch slot, batches per wave
 VFLAGS_ps1024        := -DRTX_PS_ITEMS=1024
 VFLAGS_ps256         := -DRTX_PS_ITEMS=256
 VFLAGS_ps128         := -DRTX_PS_ITEMS=128
-VFLAGS_psnostore     := -DRTX_PS_DIAG_NOSTORE=1
 VFLAGS_psb80         := -DRTX_PS_BPW=80
 VFLAGS_psb20         := -DRTX_PS_BPW=20
 # test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and

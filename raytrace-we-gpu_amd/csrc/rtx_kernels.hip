@@ -82,9 +82,6 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 #ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
 #define RTX_DIAG_PIXEL 0
 #endif
-#ifndef RTX_PS_DIAG_NOSTORE  // timing diagnostic: k_render_ps drops its sample colours (WRONG images)
-#define RTX_PS_DIAG_NOSTORE 0
-#endif
 #ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
 #define RTX_DIAG_COOP 0
 #endif
@@ -1707,9 +1704,6 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
             f3 c = mk3(0.0f, 0.0f, 0.0f);
             const int r = path_segment(P, L, min(hit, last), best, c);
             if (r != kSegContinue) {
-#if RTX_PS_DIAG_NOSTORE  // timing diagnostic only: WRONG images
-                if (c.x == 12345.0f)
-#endif
                 scr[(size_t)L.slot * P.ps_cap + L.sidx] = make_float4(c.x, c.y, c.z, 0.0f);  // +0: black path
                 atomicAdd(&st[4 * L.slot + 3], 1u);
                 L.active = false;

@@ -105,11 +105,7 @@ RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy
         T.thr = -INFINITY;
         return T;
     }
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTX_IEEE_BASIS)  // A/B only: the IEEE basis
-    const float sn = sqrtf(n2);
-    const float inv_n = 1.0f / sn;
-    const float w = 1.0f / (sqrtf(a) * sn);
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     const float inv_n = pf_rsq(n2);  // n2 >= 2^-80 and a >= 2^-40 here: normal inputs
     const float w = pf_rsq(a) * inv_n;
 #else
