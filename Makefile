@@ -45,10 +45,12 @@ clean:
 
 # Kernel variants for A/B timing (tools/variant_bench.py): same sources,
 # different compile-time choices. Not used by the product path.
-VARIANTS := best nopack lag0 lag32 every4 noflat prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psb80 psb20
+VARIANTS := best nopack w4 w6 lag0 lag32 every4 noflat prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psb80 psb20
 VFLAGS_best          :=
 VFLAGS_noflat        := -DRTX_FLAT=0
 VFLAGS_nopack        := -DRTX_PACK=0
+VFLAGS_w4            := -DRTX_WAVES_PER_SIMD=4
+VFLAGS_w6            := -DRTX_WAVES_PER_SIMD=6
 VFLAGS_lag0          := -DRTX_PACK_LAG=0
 VFLAGS_lag32         := -DRTX_PACK_LAG=32
 VFLAGS_every4        := -DRTX_PACK_EVERY=4

@@ -99,9 +99,11 @@ constexpr double kHeavy2AlphaMedium = 1.5;  // tier 2 for a medium share: key > 
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
+#ifndef RTX_WAVES_PER_SIMD
 #define RTX_WAVES_PER_SIMD 5  // occupancy request for the render kernels: 96 VGPRs (the compiler's own
                               // choice is 100: 4 waves); the few spills (SGPRs to VGPR lanes, ~7 VGPR
                               // dwords to scratch) sit in per-segment and coop code, none in the scan loop
+#endif
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
 
 // Candidate list: per lane kCand slots in LDS, slot-major
