@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
                    help="rocprofv3 PMC child passes for HBM traffic (rank 0, N=1)")
+    p.add_argument("--per-sample", type=int, default=1,
+                   help="also time the per-sample-RNG kernel on the same frame (N=1, chain runs only)")
     p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -202,6 +204,19 @@ def cpu_baseline(args, world, frame, gpu_image, budget_s):
             "host": host_cpu()}, {"rows_checked": len(done), "values_differing": mism, "bit_exact": mism == 0}
 
 
+def per_sample_parity(world, frame, img, rows):
+    """Checker for the per-sample line: a few rows of the per-sample frame
+    against the fp32 oracle in the same RNG mode (bit for bit)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16))
+    want, _ = oracle.render_rows(world, frame, np.array(rows, np.uint32), nthreads=threads)
+    got = img[rows]
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    return {"rows_checked": len(rows), "values_differing": int((~same).sum()), "bit_exact": bool(same.all())}
+
+
 def host_cpu():
     """The box's CPU: logical CPUs visible and the model name."""
     model = ""
@@ -302,6 +317,34 @@ def main():
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
             cpu, parity = cpu_baseline(args, world, frame, host_img, args.cpu_seconds)
+        # The north star's kernel shape — one lane per (pixel, sample) — on the
+        # same frame with per-(pixel, sample) seeds (rtx_frame.rng_mode 1,
+        # DESIGN.md §3a): reported beside the headline, which stays the
+        # reference's chain RNG. N = 1 only.
+        per_sample = None
+        if R == 1 and args.rng == "chain" and args.per_sample:
+            frame.rng_mode = 1
+            ctx.set_frame(frame)
+            ctx.render_rows(1, 0, 1, image.data_ptr())
+            torch.cuda.synchronize()
+            ctx.stats_reset()
+            n_ps = max(1, min(args.steps, 5))
+            t_ps = time.perf_counter()
+            for _ in range(n_ps):
+                ctx.render_rows(1, 0, 1, image.data_ptr())
+            torch.cuda.synchronize()
+            t_ps = (time.perf_counter() - t_ps) / n_ps
+            st_ps = ctx.stats()
+            ps_ms = st_ps.kernel_ms / max(1, st_ps.launches)
+            ps_flops = FLOP_PER_TEST * st_ps.sphere_tests / max(1, st_ps.launches)
+            per_sample = {"value": round(W * H * args.spp / t_ps / 1e6, 3), "unit": "Msamples/s",
+                          "ms_per_step": round(t_ps * 1e3, 3), "steps": n_ps, "kernel_ms": round(ps_ms, 4),
+                          "frac": round(ps_flops / (ps_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                          "kernel": "k_render_ps (one lane per pixel-sample, in-order fold per pixel)"}
+            if args.cpu_seconds > 0:
+                per_sample["parity"] = per_sample_parity(world, frame, image.cpu().numpy(), [H // 3, 2 * H // 3])
+            frame.rng_mode = 0
+            ctx.set_frame(frame)
         line = {
             "metric": "Msamples/sec (pixels x spp) at 1920x1080 spp=100 depth=50",
             "value": round(value, 3),
@@ -340,6 +383,7 @@ def main():
                              "traffic": None if traffic is None else round(traffic)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "per_sample_rng": per_sample,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
