@@ -95,7 +95,7 @@ constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than th
 constexpr double kHeavy1AlphaLow = 3.5;     // tier-1 bar for a low share
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
-constexpr double kHeavy2AlphaMedium = 1.5;  // tier 2 for a medium share: key > this * share
+constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > this * share (2-way split: 37 -> 34 ms, r5a-b)
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
