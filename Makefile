@@ -43,34 +43,21 @@ clean:
 
 .PHONY: all oracle asm clean
 
-# Kernel variants for A/B timing (tools/variant_bench.py): same sources,
-# different compile-time choices. Not used by the product path.
-VARIANTS := best nopack w4 w6 lag0 lag32 every4 noflat prof ptime cprof cprof2 stress cand24 cand6 pfcand12 ps1024 ps256 ps128 psb80 psb20
-VFLAGS_best          :=
-VFLAGS_noflat        := -DRTX_FLAT=0
-VFLAGS_nopack        := -DRTX_PACK=0
-VFLAGS_w4            := -DRTX_WAVES_PER_SIMD=4
-VFLAGS_w6            := -DRTX_WAVES_PER_SIMD=6
-VFLAGS_lag0          := -DRTX_PACK_LAG=0
-VFLAGS_lag32         := -DRTX_PACK_LAG=32
-VFLAGS_every4        := -DRTX_PACK_EVERY=4
+# Kernel variants (same sources, different compile-time choices; never the
+# product path):
+#   stress - candidate lists of 1 entry and coop resolve rounds of one scan
+#            step, so every overflow, round and fallback path runs all the
+#            time (tests/test_gpu_parity.py)
+#   prof   - per-section clock sums (tools/section_prof.py)
+#   ptime  - per-pixel start/end times (tools/pixel_timeline.py)
+#   cprof  - per-section clocks of tier-1 coop segments (tools/coop_prof.py)
+# Ad-hoc A/B builds for tools/variant_bench.py:
+#   make adhoc V=name VFLAGS="-DRTX_...=..."   -> lib/variants/librtx_name.so
+VARIANTS := stress prof ptime cprof
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
-VFLAGS_cprof2        := -DRTX_DIAG_COOP=2
-# candidate-list length (entries of 8 spheres per lane before a resolve round)
-VFLAGS_cand24        := -DRTX_CAND=24
-VFLAGS_cand6         := -DRTX_CAND=6
-VFLAGS_pfcand12      := -DRTX_CAND_PF=12
-# per-sample kernel: items per batch slot, batches per wave
-VFLAGS_ps1024        := -DRTX_PS_ITEMS=1024
-VFLAGS_ps256         := -DRTX_PS_ITEMS=256
-VFLAGS_ps128         := -DRTX_PS_ITEMS=128
-VFLAGS_psb80         := -DRTX_PS_BPW=80
-VFLAGS_psb20         := -DRTX_PS_BPW=20
-# test build: lists of 1 entry and 2 sphere-major pairs, so every overflow and
-# fallback path runs all the time (tests/test_gpu_parity.py, stress tests)
-VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_SM_CAND=2
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
@@ -82,4 +69,12 @@ $(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.c
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(VDIR)/$*/k.o $(VDIR)/$*/a.o $(VDIR)/$*/h.o
 
-.PHONY: variants
+adhoc:
+	@test -n "$(V)" || (echo "usage: make adhoc V=name VFLAGS=..." && false)
+	mkdir -p $(VDIR)/$(V)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$(V)/k.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_api.hip -o $(VDIR)/$(V)/a.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$(V)/h.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $(VDIR)/librtx_$(V).so $(VDIR)/$(V)/k.o $(VDIR)/$(V)/a.o $(VDIR)/$(V)/h.o
+
+.PHONY: variants adhoc

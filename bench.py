@@ -342,7 +342,8 @@ def main():
                           "frac": round(ps_flops / (ps_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
                           "kernel": "k_render_ps (one lane per pixel-sample, in-order fold per pixel)"}
             if args.cpu_seconds > 0:
-                per_sample["parity"] = per_sample_parity(world, frame, image.cpu().numpy(), [H // 3, 2 * H // 3])
+                rows_ps = [int(r) for r in np.linspace(5, H - 6, 16)]  # 16 rows spread over the image
+                per_sample["parity"] = per_sample_parity(world, frame, image.cpu().numpy(), rows_ps)
             frame.rng_mode = 0
             ctx.set_frame(frame)
         line = {

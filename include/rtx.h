@@ -38,7 +38,16 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 100 /* 1.0.0 */
+#define RTX_VERSION 110 /* 1.1.0 */
+/* ABI notes.
+ *  1.1.0: rtx_schedule_defaults / rtx_set_schedule / rtx_get_schedule (the
+ *         chain-RNG schedule, formerly an undocumented environment variable
+ *         of the library: the library now reads no environment);
+ *         rtx_debug_hit_world_from; rtx_debug_hit_world rejects t_min <= 0.
+ *  1.0.x: rtx_set_stream(ctx, NULL) selects HIP's null (legacy default)
+ *         stream, which implicitly synchronises with every blocking stream;
+ *         the context's own non-blocking stream is rtx_use_own_stream. (The
+ *         first 1.0 builds treated NULL as "own stream".) */
 
 enum {
     RTX_OK = 0,
@@ -140,6 +149,53 @@ RTX_API void rtx_destroy(rtx_ctx *ctx);
 RTX_API int rtx_set_stream(rtx_ctx *ctx, void *hip_stream);
 /* Back to the context's own non-blocking stream (the state after rtx_create). */
 RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
+
+/* ---- schedule of the chain-RNG render ------------------
+ * The reference's RNG chain makes a pixel's samples sequential, so the render
+ * schedules PIXELS: a 2-spp cost pre-pass gives every pixel a cost key (its
+ * 3x3 neighbourhood's segments), the persistent render takes pixels most
+ * expensive first, and the heaviest are traced by groups of lanes. With
+ * share = (sum of the keys) / (resident lanes) and "pixels per lane" = the
+ * part's pixels / resident lanes:
+ *   - tier 1 (one pixel per wave, 64 lanes per ray): keys above
+ *     tier1_bar x share; for a SMALL part (pixels per lane < small_share,
+ *     e.g. one rank of an 8-way split) tier1_bar_small, for a LOW part
+ *     (< low_share) tier1_bar_low;
+ *   - tier 2 (eight pixels per wave): a small part's keys above
+ *     tier2_bar_small x share, a MEDIUM part's (< medium_share) above
+ *     tier2_bar_medium x share;
+ *   - hot_fraction x resident lanes of the normal queue's first slots run at
+ *     the top wave priority;
+ *   - occupancy_*: the fraction of the resident waves launched for a small /
+ *     low / larger part;
+ *   - tail_coop_max: once the queue is empty a wave with at most this many
+ *     pixels left traces them with several lanes per ray (1..64).
+ * Results never depend on the schedule (every pixel's operations are the
+ * same whichever lanes trace it); only the time does. The defaults are the
+ * measured best. A context starts with the defaults. */
+typedef struct rtx_schedule {
+    float tier1_bar;          /* default 1.7 */
+    float tier1_bar_small;    /* default 4.0 */
+    float tier1_bar_low;      /* default 3.5 */
+    float tier2_bar_small;    /* default 2.0 */
+    float tier2_bar_medium;   /* default 1.2 */
+    float small_share;        /* default 1.2 pixels per resident lane */
+    float low_share;          /* default 2.5 */
+    float medium_share;       /* default 3.5 */
+    float hot_fraction;       /* default 0.2 */
+    float occupancy_small;    /* default 1.0; each occupancy in (0, 1] */
+    float occupancy_low;      /* default 1.0 */
+    float occupancy_normal;   /* default 1.0 */
+    uint32_t tail_coop_max;   /* default 8 */
+    uint32_t reserved;        /* must be 0 */
+} rtx_schedule;
+/* The library's defaults (no context, no GPU). */
+RTX_API int rtx_schedule_defaults(rtx_schedule *out);
+/* Validates and installs a schedule for later launches of `ctx` (NULL =
+ * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
+ * occupancies in (0, 1], tail_coop_max in 1..64, reserved 0. */
+RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
+RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 
 /* ---- scene / frame upload ----------------------------------------------
  * ~ CreateBuffer(WorldDef, IMMUTABLE) (DxCSApp.cpp:393-413). */
@@ -251,6 +307,18 @@ RTX_API int rtx_frame_from_perframe(const void *perframe_bytes, size_t nbytes,
  * Uses the uploaded world. Synchronous. ~ hit_world, ShaderCompute.hlsl:188-205. */
 RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                 float t_min, float t_max, float *out);
+/* Requirements of both: t_min finite and > 0 (the render's 0.001; the
+ * kernel orders candidate roots by their bit patterns, which order like the
+ * values only for positive roots), t_max not NaN. t_max < t_min: no ray
+ * hits (no root lies in [t_min, t_max]).
+ * rtx_debug_hit_world_from: the same, with the prefiltered scan starting at
+ * 8-sphere block start_block % ceil(count / 8) and wrapping round — the
+ * start the large-scene kernels take from their workgroup's position word
+ * (DESIGN.md §3 "pack start"); the result is the in-order scan's for every
+ * start (ties between spheres on either side of the wrap included). */
+RTX_API int rtx_debug_hit_world_from(rtx_ctx *ctx, const float *rays, uint32_t nrays,
+                                     float t_min, float t_max, uint32_t start_block,
+                                     float *out);
 /* Evaluates device math function `fn` (RTX_FN_*) elementwise on host
  * arrays (in0, in1 may be unused); out receives n floats (hash functions
  * write 1, 2 or 3 floats per element: out must hold 3*n). The diffuse

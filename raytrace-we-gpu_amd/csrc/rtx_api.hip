@@ -42,11 +42,12 @@ struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
-// Launch timing: a fixed ring of event pairs. When every pair is in use the
-// oldest launch's duration is folded into a running total (waiting for its
-// stop event, long finished in practice), so a host that renders forever
-// without rtx_stats_reset keeps kEventRing pairs, not one per launch.
-constexpr size_t kEventRing = 64;
+// Launch timing: a ring of event pairs. When every pair is in use, the
+// oldest launch's duration is folded into a running total if its stop event
+// has completed (hipEventQuery, no wait); otherwise the ring doubles. A host
+// that renders forever without rtx_stats_reset keeps as many pairs as it
+// has launches in flight, and a launch never blocks on an older one.
+constexpr size_t kEventRing = 64;  // initial ring size
 
 }  // namespace
 
@@ -90,8 +91,9 @@ struct rtx_ctx {
     // per-sample RNG kernel's per-wave sample-colour scratch
     float *d_ps = nullptr;
     size_t ps_floats = 0;
-    EventPair events[kEventRing];   // ring: [ev_head, ev_head + ev_count) outstanding
+    std::vector<EventPair> events = std::vector<EventPair>(kEventRing);  // ring: [ev_head, ev_head + ev_count)
     size_t ev_head = 0, ev_count = 0;
+    rtx::KTune tune = rtx::default_tune();  // rtx_set_schedule
     double ms_folded = 0.0;         // durations of launches whose pair was recycled
     uint64_t samples = 0;
     uint64_t launches = 0;
@@ -224,6 +226,86 @@ int rtx_use_own_stream(rtx_ctx *c) {
     return RTX_OK;
 }
 
+int rtx_schedule_defaults(rtx_schedule *out) {
+    if (!out) return fail(RTX_ERR_INVALID, "rtx_schedule_defaults: null out");
+    const rtx::KTune t = rtx::default_tune();
+    *out = rtx_schedule{};
+    out->tier1_bar = (float)t.a1;
+    out->tier1_bar_small = (float)t.a1_small;
+    out->tier1_bar_low = (float)t.a1_low;
+    out->tier2_bar_small = (float)t.a2_small;
+    out->tier2_bar_medium = (float)t.a2_medium;
+    out->small_share = (float)t.rho;
+    out->low_share = (float)t.rho_low;
+    out->medium_share = (float)t.rho2;
+    out->hot_fraction = (float)t.prio_frac;
+    out->occupancy_small = (float)t.occ_small;
+    out->occupancy_low = (float)t.occ_low;
+    out->occupancy_normal = (float)t.occ_normal;
+    out->tail_coop_max = t.coop_max;
+    return RTX_OK;
+}
+
+int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_set_schedule: null ctx");
+    if (!s) {
+        c->tune = rtx::default_tune();
+        return RTX_OK;
+    }
+    const struct { const char *name; float v; } pos[] = {
+        {"tier1_bar", s->tier1_bar},         {"tier1_bar_small", s->tier1_bar_small},
+        {"tier1_bar_low", s->tier1_bar_low}, {"tier2_bar_small", s->tier2_bar_small},
+        {"tier2_bar_medium", s->tier2_bar_medium}, {"small_share", s->small_share},
+        {"low_share", s->low_share},         {"medium_share", s->medium_share}};
+    for (const auto &f : pos)
+        if (!(f.v > 0.0f && f.v <= 1e30f))
+            return fail(RTX_ERR_INVALID, std::string("rtx_set_schedule: ") + f.name + " must be finite and > 0");
+    if (!(s->hot_fraction >= 0.0f && s->hot_fraction <= 1.0f))
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: hot_fraction must be in [0, 1]");
+    const float occ[] = {s->occupancy_small, s->occupancy_low, s->occupancy_normal};
+    for (float o : occ)
+        if (!(o > 0.0f && o <= 1.0f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: occupancies must be in (0, 1]");
+    if (s->tail_coop_max < 1 || s->tail_coop_max > 64)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max must be in 1..64");
+    if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
+    rtx::KTune t;
+    t.a1 = s->tier1_bar;
+    t.a1_small = s->tier1_bar_small;
+    t.a1_low = s->tier1_bar_low;
+    t.a2_small = s->tier2_bar_small;
+    t.a2_medium = s->tier2_bar_medium;
+    t.rho = s->small_share;
+    t.rho_low = s->low_share;
+    t.rho2 = s->medium_share;
+    t.prio_frac = s->hot_fraction;
+    t.occ_small = s->occupancy_small;
+    t.occ_low = s->occupancy_low;
+    t.occ_normal = s->occupancy_normal;
+    t.coop_max = s->tail_coop_max;
+    c->tune = t;
+    return RTX_OK;
+}
+
+int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
+    if (!c || !out) return fail(RTX_ERR_INVALID, "rtx_get_schedule: null argument");
+    const rtx::KTune &t = c->tune;
+    *out = rtx_schedule{};
+    out->tier1_bar = (float)t.a1;
+    out->tier1_bar_small = (float)t.a1_small;
+    out->tier1_bar_low = (float)t.a1_low;
+    out->tier2_bar_small = (float)t.a2_small;
+    out->tier2_bar_medium = (float)t.a2_medium;
+    out->small_share = (float)t.rho;
+    out->low_share = (float)t.rho_low;
+    out->medium_share = (float)t.rho2;
+    out->hot_fraction = (float)t.prio_frac;
+    out->occupancy_small = (float)t.occ_small;
+    out->occupancy_low = (float)t.occ_low;
+    out->occupancy_normal = (float)t.occ_normal;
+    out->tail_coop_max = t.coop_max;
+    return RTX_OK;
+}
+
 int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (!c || !w) return fail(RTX_ERR_INVALID, "rtx_upload_world: null argument");
     if (w->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_upload_world: reserved must be 0");
@@ -272,7 +354,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     float smag_f = (float)smag;
     if ((double)smag_f < smag) smag_f = std::nextafter(smag_f, INFINITY);
     // The longest run of flat blocks (rtx_prefilter.h: all 8 centre heights
-    // equal, bit for bit, and equal along the run): the scan's 6-op test.
+    // equal, bit for bit, and equal along the run): the scan's 5-op test.
     uint32_t flat_lo = 0, flat_hi = 0;
     float flat_cy = 0.0f;
     {
@@ -467,16 +549,25 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     }
     rtx::KParams p = make_params(c, rows, tile_rows, part, nparts, out, accum, accum_frames, frame_index);
 
-    if (c->ev_count == kEventRing) {  // recycle the oldest pair: fold its duration
+    if (c->ev_count == c->events.size()) {
         EventPair &old = c->events[c->ev_head];
-        RTX_HIP(hipEventSynchronize(old.stop));
-        float t = 0.0f;
-        RTX_HIP(hipEventElapsedTime(&t, old.start, old.stop));
-        c->ms_folded += t;
-        c->ev_head = (c->ev_head + 1) % kEventRing;
-        c->ev_count--;
+        const hipError_t q = hipEventQuery(old.stop);
+        if (q == hipSuccess) {  // recycle the oldest pair: fold its duration
+            float t = 0.0f;
+            RTX_HIP(hipEventElapsedTime(&t, old.start, old.stop));
+            c->ms_folded += t;
+            c->ev_head = (c->ev_head + 1) % c->events.size();
+            c->ev_count--;
+        } else if (q == hipErrorNotReady) {  // still running: grow the ring, no wait
+            std::vector<EventPair> grown(2 * c->events.size());
+            for (size_t i = 0; i < c->ev_count; ++i) grown[i] = c->events[(c->ev_head + i) % c->events.size()];
+            c->events.swap(grown);
+            c->ev_head = 0;
+        } else {
+            return hip_fail(q, "hipEventQuery");
+        }
     }
-    EventPair &ev = c->events[(c->ev_head + c->ev_count) % kEventRing];
+    EventPair &ev = c->events[(c->ev_head + c->ev_count) % c->events.size()];
     if (!ev.start) RTX_HIP(hipEventCreate(&ev.start));
     if (!ev.stop) RTX_HIP(hipEventCreate(&ev.stop));
     RTX_HIP(hipEventRecord(ev.start, c->stream));
@@ -508,6 +599,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     sched.state = reinterpret_cast<float4 *>(c->d_sched + sched_state_off(c->sched_pixels));
     sched.npix = (uint32_t)c->sched_pixels;
     sched.nbuckets = rtx::kCostBuckets;
+    sched.tune = c->tune;
     hipError_t e = rtx::launch_render(p, sched, c->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_render");
     RTX_HIP(hipEventRecord(ev.stop, c->stream));
@@ -581,7 +673,7 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     RTX_HIP(hipStreamSynchronize(c->stream));
     double ms = c->ms_folded;
     for (size_t i = 0; i < c->ev_count; ++i) {
-        const EventPair &p = c->events[(c->ev_head + i) % kEventRing];
+        const EventPair &p = c->events[(c->ev_head + i) % c->events.size()];
         float t = 0.0f;
         RTX_HIP(hipEventElapsedTime(&t, p.start, p.stop));
         ms += t;
@@ -681,24 +773,41 @@ int rtx_debug_wave_times(rtx_ctx *c, size_t max_waves, unsigned long long *host_
     return RTX_OK;
 }
 
-int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_min, float t_max,
-                        float *out) {
+int rtx_debug_hit_world_from(rtx_ctx *c, const float *rays, uint32_t nrays, float t_min, float t_max,
+                             uint32_t start_block, float *out) {
     if (!c || (nrays && (!rays || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_hit_world: null argument");
     if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_debug_hit_world: no world uploaded");
+    // the resolve compares roots by their bit patterns (rtx_kernels.hip
+    // hit_key), which order like the values only for roots > 0
+    if (!(t_min > 0.0f && t_min <= 3.4e38f))
+        return fail(RTX_ERR_INVALID, "rtx_debug_hit_world: t_min must be finite and > 0");
+    if (t_max != t_max) return fail(RTX_ERR_INVALID, "rtx_debug_hit_world: t_max is NaN");
     if (nrays == 0) return RTX_OK;
+    if (t_max < t_min) {  // no root lies in [t_min, t_max]: every ray misses
+        for (size_t i = 0; i < (size_t)nrays; ++i) {
+            for (int k = 0; k < 9; ++k) out[10 * i + k] = 0.0f;
+            out[10 * i + 9] = -1.0f;
+        }
+        return RTX_OK;
+    }
     int rc = set_device(c);
     if (rc) return rc;
     float *d_rays = nullptr, *d_out = nullptr;
     RTX_HIP(hipMalloc(&d_rays, (size_t)nrays * 6 * sizeof(float)));
     hipError_t e = hipMalloc(&d_out, (size_t)nrays * 10 * sizeof(float));
     if (e == hipSuccess) e = hipMemcpyAsync(d_rays, rays, (size_t)nrays * 6 * sizeof(float), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = rtx::launch_debug_hit_world(scene_of(c), d_rays, nrays, t_min, t_max, d_out, c->stream);
+    if (e == hipSuccess)
+        e = rtx::launch_debug_hit_world(scene_of(c), d_rays, nrays, t_min, t_max, start_block, d_out, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, (size_t)nrays * 10 * sizeof(float), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d_rays);
     (void)hipFree(d_out);
     if (e != hipSuccess) return hip_fail(e, "rtx_debug_hit_world");
     return RTX_OK;
+}
+
+int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_min, float t_max, float *out) {
+    return rtx_debug_hit_world_from(c, rays, nrays, t_min, t_max, 0, out);
 }
 
 int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint32_t n, float *out) {

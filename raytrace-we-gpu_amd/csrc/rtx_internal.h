@@ -22,7 +22,7 @@ namespace rtx {
 //                         array every ray segment scans
 // `smag` bounds |c| + r over the scene (rounded up), for the prefilter's
 // per-ray overflow guard. Blocks [flat_lo, flat_hi) of `pre` hold spheres
-// whose centres all have height flat_cy (the scan's 6-op test,
+// whose centres all have height flat_cy (the scan's 5-op test,
 // rtx_prefilter.h line_test_q_flat).
 struct KScene {
     const float *soa;
@@ -78,6 +78,17 @@ struct KParams {
 // count; a counting sort orders the pixel queue by that cost, descending,
 // so the pixels that take longest start first and the frame does not end
 // on a few expensive pixels started late.
+// The chain render's schedule (include/rtx.h rtx_schedule; validated by
+// rtx_set_schedule): heavy-pixel tier bars, share classes, hot-wave
+// fraction, launch occupancy, tail-coop size. Doubles: k_heavy_split
+// compares them with sums of cost keys.
+struct KTune {
+    double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
+    double occ_small, occ_low, occ_normal;  // fraction of the resident waves launched for a small / low / larger share
+    uint32_t coop_max;                      // KParams::coop_max
+};
+KTune default_tune();
+
 struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
@@ -87,6 +98,7 @@ struct KSchedule {
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
     float *ps_scratch;  // k_render_ps scratch (rng_mode 1), ps_floats floats
     size_t ps_floats;
+    KTune tune;
 };
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
@@ -103,7 +115,8 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
                                uint32_t height, uint32_t tile_rows, uint32_t nparts,
                                uint32_t max_rows, hipStream_t stream);
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays,
-                                  float t_min, float t_max, float *out, hipStream_t stream);
+                                  float t_min, float t_max, uint32_t start_block, float *out,
+                                  hipStream_t stream);
 hipError_t launch_debug_math(int fn, const float *in0, const float *in1, uint32_t n,
                              float *out, hipStream_t stream);
 

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "rtx_device_math.h"
+#include "rtx_diag.h"
 #include "rtx_internal.h"
 #include "rtx_prefilter.h"
 
@@ -73,18 +74,10 @@ __device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_
 // a = |d|^2 (Sphere.cpp:8; HLSL length(d)*length(d), :160), fma form.
 __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y, d.y, d.x * d.x)); }
 
-// Compile-time knobs. The diagnostics are separate builds (Makefile
-// variants prof/ptime/cprof); the candidate-list capacities below are also
-// set by the stress build. Everything else is a fixed product constant.
-#ifndef RTX_DIAG_PROF  // diagnostic: per-section clock sums into the wave_times buffer
-#define RTX_DIAG_PROF 0
-#endif
-#ifndef RTX_DIAG_PIXEL  // diagnostic: per-pixel (start | mode, end) s_memrealtime into wave_times[2*gid..]
-#define RTX_DIAG_PIXEL 0
-#endif
-#ifndef RTX_DIAG_COOP  // diagnostic: per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
-#define RTX_DIAG_COOP 0
-#endif
+// Compile-time knobs. The diagnostics are separate builds (rtx_diag.h;
+// Makefile variants prof/ptime/cprof); the candidate-list capacities below
+// are also set by the stress build. Everything else is a fixed product
+// constant.
 constexpr int kCoopMax = 8;             // tail mode: a wave with <= this many active lanes traces their rays together
 constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wave
 constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
@@ -126,22 +119,7 @@ template <bool kPF>
 constexpr uint32_t list_bytes() { return (cand_of<kPF>() + 1) * kRB * sizeof(uint32_t); }
 static_assert(list_bytes<true>() % 16 == 0 && RTX_CAND_PF >= 1, "LDS carve must stay 16-byte aligned");
 
-#if RTX_DIAG_PROF
-// Diagnostic event counters, one set per wave in LDS: [0] batches scanned
-// [1] batches recorded (some lane had a candidate) [2] resolve iterations
-// [3] lanes falling back to the in-order scan [4] candidate entries (lanes)
-__device__ __forceinline__ uint32_t *diag_slots() {
-    __shared__ uint32_t s[kRB / 64][8];
-    return s[threadIdx.x / 64];
-}
-__device__ __forceinline__ void diag_add(int k, uint32_t v) {
-    const uint64_t m = __ballot(1);
-    if ((int)(threadIdx.x & 63u) == __ffsll((long long)m) - 1) diag_slots()[k] += v;
-}
-#define RTX_DIAG_ADD(k, v) diag_add(k, v)
-#else
-#define RTX_DIAG_ADD(k, v)
-#endif
+static_assert(kRB / 64 == 4, "rtx_diag.h keeps 4 waves per workgroup");
 
 // Roots of a sphere whose disc >= 0 (or NaN): near root first, far root if
 // the near one is outside [t_min, best] (Sphere.cpp:15-24); strict
@@ -223,7 +201,7 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // kPF (scenes above kScanPfMin): the block's 32 floats are double-buffered in SGPRs. The
 // next block's two s_load_dwordx16 are issued (inline asm: the compiler
 // otherwise sinks them to the end of the iteration and waits at once) before
-// this block's 33 VALU instructions and waited for after them, so a scalar
+// this block's ~25 VALU instructions and waited for after them, so a scalar
 // cache miss (every block of a large scene) runs under the block's compute.
 // Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
 // loaded registers ("+s") so that nothing reads them before it. Every path
@@ -253,15 +231,19 @@ __device__ __forceinline__ void sload_blk(cfloat_p p, f16v &lo, f16v &hi, f2v &d
 __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(lo), "+s"(hi));
 }
-// One run of blocks [b, end), all flat (kFlat: the 6-op test, kvn = kv)
-// or not (kvn = -(o.v)). Returns the block to resume at; `full` when it
-// stopped because some lane's list is full.
+// One run of blocks [b, end), all flat (kFlat: the 5-op test, k0/k1 = the
+// per-ray ku/kv of rtx_prefilter.h line_test_flat) or not (the 7-op test,
+// k0/k1 = nou/nov). Returns the block to resume at; `full` when it stopped
+// because some lane's list is full.
+#ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
+#define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
+#endif
 template <bool kPF, bool kFlat>
 __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_t end, const LineTest &T,
-                                               float kvn1, uint32_t *my, uint32_t &cnt, bool &full,
-                                               uint32_t *pack) {
-    f2v ux = {T.ux, T.ux}, uz = {T.uz, T.uz}, vx = {T.vx, T.vx}, vy = {T.vy, T.vy};
-    f2v vz = {T.vz, T.vz}, nou = {T.nou, T.nou}, kvn = {kvn1, kvn1};
+                                               float k0, float k1, uint32_t *my, uint32_t &cnt, bool &full,
+                                               uint32_t *pack, const float *lds_pr) {
+    f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy};
+    f2v vz = {T.vz, T.vz}, ku = {k0, k0}, kv = {k1, k1};
     const f2v th = {T.thr, T.thr};
     // One 8-sphere block (blk(i) = its i-th float); true when some lane's
     // list is full and the scan must stop after this block.
@@ -272,13 +254,14 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             const f2v cx = {blk(2 * p), blk(2 * p + 1)};
             const f2v cz = {blk(16 + 2 * p), blk(17 + 2 * p)};
             const f2v R = {blk(24 + 2 * p), blk(25 + 2 * p)};
-            const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
-            f2v pv;
-            if constexpr (kFlat) {
-                pv = fma2(cx, vx, fma2(cz, vz, kvn));
-            } else {
+            f2v pu, pv;
+            if constexpr (kFlat) {  // line_test_q_flat: c.v - o.v is one fma
+                pu = fma2(cx, ux, fma2(cz, uz, ku));
+                pv = fma2(cz, vz, kv);
+            } else {                // line_test_q
                 const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
-                pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, kvn)));
+                pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, ku)));
+                pv = fma2(cy, vy, fma2(cz, vz, kv));
             }
             q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
         }
@@ -309,10 +292,10 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
     if constexpr (kPF) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
         f16v a_lo, a_hi, b_lo, b_hi;
-        sload_blk(pre + 32 * b, a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
+        sload_blk(pre + 32 * b, a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
         sload_wait(a_lo, a_hi);
         for (;;) {
-            sload_blk(pre + 32 * min(b + 1, end - 1), b_lo, b_hi, ux, uz, vx, vy, vz, nou, kvn);
+            sload_blk(pre + 32 * min(b + 1, end - 1), b_lo, b_hi, ux, uy, uz, vy, vz, ku, kv);
             bool f = step([&](int i) { return i < 16 ? a_lo[i] : a_hi[i - 16]; }, b);
             sload_wait(b_lo, b_hi);
             if (f) return b + 1;
@@ -325,16 +308,32 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             // scan) measured no faster than no pack at all, this 4-7 % faster
             // (DESIGN.md §7 R4k-q).
             if (RTX_PACK && (b & (kPackEvery - 1u)) == 0u && (threadIdx.x & 63u) == 0u) *pack = b;
-            sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uz, vx, vy, vz, nou, kvn);
+            sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
             f = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
             sload_wait(a_lo, a_hi);
             if (f) return b + 1;
             if (++b >= end) break;
         }
     } else {
-        for (; b < end; ++b) {
-            const cfloat_p blk = pre + 32 * b;
-            if (step([&](int i) { return blk[i]; }, b)) return b + 1;
+        if (RTX_SCAN_LDS && lds_pr) {
+            for (; b < end; ++b) {  // pair p of block b: [cx0 cx1 cy0 cy1 cz0 cz1 R0 R1] (SphLds)
+                const float4 *q = reinterpret_cast<const float4 *>(lds_pr + 32u * b);
+                float4 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = q[t];
+                auto blk = [&](int i) {  // AoSoA-8 float i of the block
+                    const int c = i >> 3, sp = i & 7, pp = sp >> 1, w = sp & 1;
+                    const float4 A = v[2 * pp], B = v[2 * pp + 1];
+                    const float a = w ? A.y : A.x, bb = w ? A.w : A.z, cc = w ? B.y : B.x, dd = w ? B.w : B.z;
+                    return c == 0 ? a : c == 1 ? bb : c == 2 ? cc : dd;
+                };
+                if (step(blk, b)) return b + 1;
+            }
+        } else {
+            for (; b < end; ++b) {
+                const cfloat_p blk = pre + 32 * b;
+                if (step([&](int i) { return blk[i]; }, b)) return b + 1;
+            }
         }
     }
     full = false;
@@ -342,24 +341,24 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
 }
 
 // The scan over blocks [b, nblk): the scene's flat run [flat_lo, flat_hi)
-// (rtx_internal.h KScene) with the 6-op test, the rest with the 7-op one.
+// (rtx_internal.h KScene) with the 5-op test, the rest with the 7-op one.
 // Returns the block to resume at: nblk, or earlier once some lane's list is
 // full (wave-uniform). kPF scans publish their position to `pack` (below).
 template <bool kPF>
 __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk, const LineTest &T,
                                                    const KScene &S, uint32_t *list, uint32_t &cnt,
-                                                   uint32_t *pack = nullptr) {
+                                                   uint32_t *pack = nullptr, const float *lds_pr = nullptr) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
-    const float kv = line_test_kv(T, S.flat_cy);
+    const LineFlat K = line_test_flat(T, S.flat_cy);
     while (b < nblk) {
         bool full;
         if (b < S.flat_lo) {
-            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nov, my, cnt, full, pack);
+            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         } else if (b < S.flat_hi) {
-            b = scan_range<kPF, true>(pre, b, min(S.flat_hi, nblk), T, kv, my, cnt, full, pack);
+            b = scan_range<kPF, true>(pre, b, min(S.flat_hi, nblk), T, K.ku, K.kv, my, cnt, full, pack, lds_pr);
         } else {
-            b = scan_range<kPF, false>(pre, b, nblk, T, T.nov, my, cnt, full, pack);
+            b = scan_range<kPF, false>(pre, b, nblk, T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         }
         if (full) break;
     }
@@ -476,16 +475,19 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // in-order answer — so the workgroup's waves stream the 100k-sphere array
 // together and a block one wave brought into the scalar cache serves the
 // waves that trail it, instead of every wave missing on every block.
+// start (no pack word): the block to start at (rtx_debug_hit_world_from),
+// wave-uniform.
 template <bool kPF, typename Ld>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
-                                                float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr) {
+                                                float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
+                                                uint32_t start = 0, const float *lds_pr = nullptr) {
     const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const float best0 = best;
     int idx = -1;
     bool ok = true;
-    uint32_t b0 = 0;
+    uint32_t b0 = nblk ? start % nblk : 0u;
     if (RTX_PACK && kPF && pack) {
         const uint32_t at = __builtin_amdgcn_readfirstlane(*pack);  // wave-uniform (SGPR)
         b0 = at < nblk ? (at + nblk - kPackLag) % nblk : 0u;  // nblk > 128 > kPackLag
@@ -493,7 +495,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     uint32_t b = b0, end = nblk;
     for (;;) {
         uint32_t cnt;
-        b = scan_prefilter<kPF>(pre, b, end, T, S, list, cnt, pack);
+        b = scan_prefilter<kPF>(pre, b, end, T, S, list, cnt, pack, lds_pr);
         ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
         if (b < end) continue;
         if (end == nblk && b0 != 0u) {  // wrap round to the start
@@ -512,28 +514,106 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
 }
 template <bool kPF>
 __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
-                                             float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr) {
+                                             float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
+                                             uint32_t start = 0) {
     const float4 *__restrict__ cen = S.cen;
-    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list, pack);
+    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list, pack,
+                                 start);
 }
 
-// ---- group-cooperative hit_world (frame tail) ------------------------------
+// ---- group-cooperative hit_world (frame tail, heavy tiers) -----------------
 // Once the pixel queue is empty a wave runs on until its last pixel ends,
-// and the frame ends on the most expensive pixels. With m <= kCoopMax
-// rays left, the wave traces them together: ray r (the r-th active lane)
-// by the g = 64 / 2^ceil(log2 m) lanes [r*g, r*g + g). Lane k of a group
-// runs the prefilter over spheres k, k+g, ... (pre4), resolves what it
-// flagged with the reference's ops (resolve_pre), and the group reduces
-// (min c, largest index): the order-independent rule of the deferred
-// resolution, hence the in-order scan's answer. The ray's own lane reads the
-// result back through LDS. A non-finite root in the group sends the ray to
-// the exact sequential path (`seq`).
-constexpr uint32_t kCoopSlots = 32;                                   // rays per wave in coop mode
-constexpr uint32_t kCoopWaveBytes = kCoopSlots * 10 * sizeof(float);  // ray (8 floats) + 64-bit key
+// and the frame ends on the most expensive pixels; the heaviest pixels of a
+// frame share (k_heavy_split) are its critical path from the start. Such
+// rays are traced together, several lanes per ray (hit_world_groups).
+//
+// Sphere sources. Scenes up to kCoopLds spheres keep a block-wide LDS copy
+// (SphLds): AoSoA-2, pair p = spheres 2p and 2p + 1 as [cx0 cx1 cy0 cy1 cz0
+// cz1 R0 R1] (R: the prefilter's inflated r^2, rtx_prefilter.h), padded to a
+// multiple of kCoopPad spheres with copies of sphere n - 1, then the radii.
+// A pair is two 16-byte LDS reads that land in the register pairs
+// v_pk_fma_f32 takes; consecutive lanes read consecutive pairs (no bank
+// conflicts). Larger scenes read the same pairs from `pre` (AoSoA-8) and the
+// resolve's (centre, radius) from `cen` (SphGlobal). A padded copy computes
+// the same roots as sphere n - 1 and can only win where it would (later
+// index wins ties): callers clamp the winner to n - 1 (rtx_internal.h).
+constexpr uint32_t kCoopSlots = 32;                                   // rays per wave in coop mode (LDS slots)
+constexpr uint32_t kCoopWaveBytes = kCoopSlots * 10 * sizeof(float);  // per-wave coop scratch (1280 B)
 constexpr uint32_t kCoopBytes = (kRB / 64) * kCoopWaveBytes;
-constexpr uint32_t kCoopStep = 2;  // spheres per coop scan step (reads in flight)
-constexpr uint32_t kCoopLds = 704;  // scenes up to this many spheres keep pre4 + radii in LDS for the coop (<= 13.75 KiB: 5 blocks/CU)
+constexpr uint32_t kCoopLds = 640;  // scenes up to this many spheres keep the coop's LDS copy (<= 12.5 KiB: 5 blocks/CU)
+constexpr uint32_t kCoopPad = 128;  // the LDS copy's sphere count is padded to a multiple of this
 static_assert(kCoopMax <= (int)kCoopSlots, "kCoopMax must be <= 32");
+__host__ __device__ constexpr uint32_t coop_npad(uint32_t n) { return (n + kCoopPad - 1u) / kCoopPad * kCoopPad; }
+__host__ __device__ constexpr uint32_t coop_lds_bytes(uint32_t n) {
+    return coop_npad(n) * 4u * (uint32_t)sizeof(float) + n * (uint32_t)sizeof(float);
+}
+static_assert(coop_lds_bytes(kCoopLds) <= 12800, "LDS copy of the scene: 5 render blocks per CU");
+
+struct SphLds {
+    static constexpr bool kPadded = true;  // npairs is a multiple of 64: every group's steps stay inside
+    const float *pr;   // [npairs][8]
+    const float *rad;  // [n]
+    uint32_t n, npairs;
+    __device__ __forceinline__ void pair(uint32_t p, f2v &cx, f2v &cy, f2v &cz, f2v &R) const {
+        const float4 *q = reinterpret_cast<const float4 *>(pr + 8u * p);
+        const float4 a = q[0], b = q[1];
+        cx = f2v{a.x, a.y};
+        cy = f2v{a.z, a.w};
+        cz = f2v{b.x, b.y};
+        R = f2v{b.z, b.w};
+    }
+    // (centre, radius) of sphere j for the resolve: the same floats as cen[j]
+    __device__ __forceinline__ float4 sphere(uint32_t j) const {
+        const float *q = pr + 8u * (j >> 1) + (j & 1u);
+        return make_float4(q[0], q[2], q[4], rad[min(j, n - 1u)]);
+    }
+};
+struct SphGlobal {
+    static constexpr bool kPadded = false;  // pair indices are clamped to npairs - 1
+    const float *pre;   // AoSoA-8, n_pad spheres
+    const float4 *cen;  // [n]
+    uint32_t n, npairs; // npairs = n_pad / 2
+    __device__ __forceinline__ void pair(uint32_t p, f2v &cx, f2v &cy, f2v &cz, f2v &R) const {
+        const float *b = pre + 32u * (p >> 2) + 2u * (p & 3u);
+        cx = *reinterpret_cast<const f2v *>(b);
+        cy = *reinterpret_cast<const f2v *>(b + 8);
+        cz = *reinterpret_cast<const f2v *>(b + 16);
+        R = *reinterpret_cast<const f2v *>(b + 24);
+    }
+    __device__ __forceinline__ float4 sphere(uint32_t j) const { return cen[min(j, n - 1u)]; }
+};
+
+// Build the block's LDS copy (all threads of the block; the caller
+// synchronises): sphere i < npad at pair i/2, slot i%2 (copies of n - 1
+// beyond n), radii after the pairs.
+__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on) {
+    SphLds l;
+    l.n = S.n;
+    l.npairs = coop_npad(S.n) / 2u;
+    l.pr = base;
+    l.rad = base + 8u * l.npairs;
+    if (on) {
+        float *pr = base, *rad = base + 8u * l.npairs;
+        for (uint32_t i = threadIdx.x; i < 2u * l.npairs; i += kRB) {
+            const float4 c = S.pre4[min(i, S.n - 1u)];
+            float *q = pr + 8u * (i >> 1) + (i & 1u);
+            q[0] = c.x;
+            q[2] = c.y;
+            q[4] = c.z;
+            q[6] = c.w;
+            if (i < S.n) rad[i] = S.cen[i].w;
+        }
+    }
+    return l;
+}
+__device__ __forceinline__ SphGlobal sph_global(const KScene &S) {
+    SphGlobal g;
+    g.pre = S.pre;
+    g.cen = S.cen;
+    g.n = S.n;
+    g.npairs = S.n_pad / 2u;
+    return g;
+}
 
 // Reduction over aligned groups of 2^lg lanes (lg wave-uniform, whole wave
 // active): DPP inside a row of 16 (quad_perm xor 1 and xor 2, then the
@@ -552,227 +632,47 @@ __device__ __forceinline__ uint32_t group_reduce_u32(uint32_t v, uint32_t lg) {
     return v;
 }
 
-__device__ __forceinline__ float read_lane(float x, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
-}
-// (Reading the tier-1 ray itself with readlane instead of through LDS costs
-// 4 VGPRs in this kernel: 98, one wave per SIMD less.)
-
-// Rays go through the wave's LDS slot; results too, except for kOne (a
-// single ray, tier 1): its line is then kept in scalars and its result,
-// left in every lane by the reduction, is read directly. rad != nullptr: sph4 and rad are the block's LDS copies
-// (resolve reads them instead of S.cen).
-#define RTX_CP(k)                                                   \
-    if (RTX_DIAG_COOP && cp) {                                      \
-        const unsigned long long tn = __builtin_readcyclecounter(); \
-        cp[k] += tn - *tq;                                          \
-        *tq = tn;                                                   \
-    }
-template <bool kOne, typename Q4>
-__device__ __forceinline__ int groups_impl(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,
-                                           f3 o, f3 d, float a, float inv_a, float t_min, float *ws,
-                                           uint32_t *list, float &best, bool &seq, unsigned long long *cp,
-                                           unsigned long long *tq) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t m = kOne ? 1u : (uint32_t)__popcll(act);
-    const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
-    const uint32_t g = 1u << lg;
-    uint32_t rank;
-    uint32_t *keys = reinterpret_cast<uint32_t *>(ws + 8 * kCoopSlots);
-    rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-    if (active) {
-        float *w = ws + 8 * rank;
-        w[0] = o.x;
-        w[1] = o.y;
-        w[2] = o.z;
-        w[3] = d.x;
-        w[4] = d.y;
-        w[5] = d.z;
-        w[6] = a;
-        w[7] = inv_a;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t r = lane >> lg, k = lane & (g - 1u);
-    const bool valid = r < m;
-    // the group's ray (LDS: re-read where needed, fewer live VGPRs)
-    const float *w = ws + 8 * (valid ? r : 0u);
-    LineTest T = line_test_setup(w[0], w[1], w[2], w[3], w[4], w[5], w[6], S.smag);
-    if constexpr (kOne) {  // uniform: keep the line in SGPRs
-        T.ux = read_lane(T.ux, 0);
-        T.uz = read_lane(T.uz, 0);
-        T.vx = read_lane(T.vx, 0);
-        T.vy = read_lane(T.vy, 0);
-        T.vz = read_lane(T.vz, 0);
-        T.nou = read_lane(T.nou, 0);
-        T.nov = read_lane(T.nov, 0);
-        T.thr = read_lane(T.thr, 0);
-    }
-    RTX_CP(0)
-    const uint32_t n = S.n;
-    // lane k of a group scans the contiguous chunk [k*ch, k*ch + ch) of the
-    // spheres (ch odd, so the group's LDS reads fall in different banks),
-    // kCoopStep spheres per step with all their reads issued before the tests
-    const uint32_t ch = ((n + g - 1u) >> lg) | 1u;
-    const uint32_t i1 = valid ? min((k + 1u) * ch, n) : 0u;
-    uint32_t i = valid ? min(k * ch, n) : 0u;
-    uint32_t *my = list + threadIdx.x;
-    float bc = __uint_as_float(0x7f800000u);
-    int bg = -1;
-    bool ok = true;
-    if constexpr (kOne) {
-        // one ray: a flagged sphere is resolved on the spot (a handful per
-        // ray), no candidate list
-        const f3 ro = mk3(read_lane(w[0], 0), read_lane(w[1], 0), read_lane(w[2], 0));
-        const f3 rd = mk3(read_lane(w[3], 0), read_lane(w[4], 0), read_lane(w[5], 0));
-        const float ra = read_lane(w[6], 0), ria = read_lane(w[7], 0);
-        for (;;) {
-            const bool more = i < i1;
-            if (__ballot(more) == 0ull) break;
-            float4 pq[kCoopStep];
-#pragma unroll
-            for (uint32_t u = 0; u < kCoopStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
-#pragma unroll
-            for (uint32_t u = 0; u < kCoopStep; ++u) {
-                const uint32_t j = i + u;
-                if (j < i1 && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr)) {
-                    const float rr = rad ? rad[j] : S.cen[j].w;
-                    uint64_t key = hit_key(bc, bg);
-                    resolve_one(make_float4(pq[u].x, pq[u].y, pq[u].z, rr), (int)j, true, ro, rd, ra, ria, t_min,
-                                key, ok);
-                    key_hit(key, bc, bg);
-                }
-            }
-            i = more ? i + kCoopStep : i;
-        }
-    } else do {
-        uint32_t cnt = 0;
-        for (;;) {
-            const bool more = i < i1;
-            if (__ballot(more) == 0ull) break;
-            float4 pq[kCoopStep];
-#pragma unroll
-            for (uint32_t u = 0; u < kCoopStep; ++u) pq[u] = sph4[min(i + u, n - 1u)];
-            uint32_t mask = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < kCoopStep; ++u)
-                if (i + u < i1 && !(line_test_q(T, pq[u].x, pq[u].y, pq[u].z, pq[u].w) < T.thr)) mask |= 1u << u;
-            if (mask != 0u) {
-                my[cnt * kRB] = i | (mask << 24);  // spheres i + bit: resolve_pre's entry format
-                ++cnt;
-            }
-            i = more ? i + kCoopStep : i;
-            if (__ballot(cnt == (uint32_t)kCand) != 0ull) break;
-        }
-        const f3 ro = mk3(w[0], w[1], w[2]), rd = mk3(w[3], w[4], w[5]);
-        if (rad)
-            ok = resolve_pre_t(
-                     [sph4, rad](uint32_t j) {
-                         const float4 q = sph4[j];
-                         return make_float4(q.x, q.y, q.z, rad[j]);
-                     },
-                     n, list, cnt, ro, rd, w[6], w[7], t_min, bc, bg) &&
-                 ok;
-        else
-            ok = resolve_pre(S.cen, n, list, cnt, ro, rd, w[6], w[7], t_min, bc, bg) && ok;
-    } while (__ballot(i < i1) != 0ull);
-    RTX_CP(1)
-    // the group's (min c, then the largest index among equal c): the rule of
-    // the in-order scan. c >= t_min > 0, so its bits order like its value.
-    const uint32_t cb0 = bg >= 0 ? __float_as_uint(bc) : 0x7f800000u;
-    const uint32_t cb = group_reduce_u32<false>(cb0, lg);
-    const uint32_t ib = group_reduce_u32<true>(bg >= 0 && cb0 == cb ? (uint32_t)bg + 1u : 0u, lg);
-    const uint64_t badm = __ballot(!ok);
-    seq = false;
-    if constexpr (kOne) {
-        RTX_CP(2)
-        if (!active) return -1;
-        if (badm != 0ull) {  // a non-finite root: the exact sequential path
-            seq = true;
-            return -1;
-        }
-        if (ib == 0u) return -1;
-        const float c = __uint_as_float(cb);
-        if (!(c <= best)) return -1;  // accepted iff c <= t_max
-        best = c;
-        return (int)(ib - 1u);
-    } else {
-        if (valid && k == 0u) {
-            const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
-            // 0: a non-finite root in the group; ~0: no hit
-            const uint64_t out = (badm & gm) != 0ull ? 0ull
-                                 : ib == 0u      ? ~0ull
-                                                 : ((uint64_t)cb << 32) | (uint64_t)(0xffffffffu - (ib - 1u));
-            keys[2 * r] = (uint32_t)out;
-            keys[2 * r + 1] = (uint32_t)(out >> 32);
-        }
-        __builtin_amdgcn_wave_barrier();
-        RTX_CP(2)
-        if (!active) return -1;
-        const uint64_t kk = ((uint64_t)keys[2 * rank + 1] << 32) | keys[2 * rank];
-        if (kk == 0ull) {
-            seq = true;
-            return -1;
-        }
-        if (kk == ~0ull) return -1;
-        const float c = __uint_as_float((uint32_t)(kk >> 32));
-        if (!(c <= best)) return -1;
-        best = c;
-        return (int)(0xffffffffu - (uint32_t)kk);
-    }
-}
-
-
-// Sphere-major group coop for kCoopSm..64 rays (tier 2 and the frame tail).
-// The per-ray groups above give each lane one ray and a long run of spheres
-// (61 for 8 rays at C2), tested two at a time: latency-bound. Here lane l
-// tests spheres l, l+64, ... against every ray in turn, two rays per packed
-// instruction (the pair's lines in SGPRs, the sphere broadcast in both
-// halves: 3.5 v_pk_fma_f32 per test, the sphere read from LDS once per pair),
-// appends each flagged (sphere, ray) pair to a wave list, and the wave then
-// resolves the list, pairs spread over all lanes, with the reference's ops
-// (the body of resolve_one); every accepted root is folded into its ray's
-// key with an LDS atomic min on (c bits << 32 | ~index), the (min c,
-// largest index) rule of the in-order scan. The rays go in chunks of
-// kSmRays (ranks [8c, 8c + 8)), one scan + resolve per chunk: a wave of
-// m rays costs ~m/64 of a lane-mode segment in its scan, so a sparse wave
-// (few pixels left, queue empty) runs its segments faster and leaves the
-// SIMD to the others. A non-finite root, or a list overflow (more than
-// kSmCand pairs in a chunk: an unsafe line flags every sphere), sends the
-// ray (the chunk's rays) to the exact sequential path. LDS per wave
-// (coop_ws, 1280 B): rays [8][8] floats, lines [8][8], keys [8] u64,
-// bad [8], count, pairs [kSmCand].
-constexpr int kCoopSm = 4;  // multi-ray coop waves with at least this many rays use groups_sm
-#ifndef RTX_SM_CAND  // sphere-major coop: (sphere, ray) pairs per chunk before the exact fallback
-#define RTX_SM_CAND 160
+// Group coop (the frame tail, tier 1 and tier 2; any ray count). The rays
+// go in chunks of at most kGfRays; a chunk of m rays gives ray r the
+// g = 64 / 2^ceil(log2 m) lanes [r*g, r*g + g), and lane k of a group tests
+// sphere pairs k, k + g, k + 2g, ... (src.pair) as v_pk_fma_f32 pairs
+// (line_test_q's ops per element; the 7-op test). The pairs a wave reads
+// at one step are g consecutive ones, the same g for every group: a
+// broadcast, conflict-free LDS read, or coalesced lines. A step's flags
+// go into a per-lane 32-bit mask (16 steps per round); each round's flagged
+// spheres are resolved with the reference's ops (resolve_one), one per lane
+// per iteration, and the group reduces (min c, then the largest index among
+// equal c) with DPP: the in-order scan's answer (deferral).
+// A non-finite root in a group sends its ray to the exact sequential path
+// (`seq`). Per ray-segment this issues about as many instructions as a
+// lane-mode segment (the scan's lane-ops are split, not repeated), at a
+// fraction of its latency.
+constexpr uint32_t kGfRays = 32;    // rays per chunk (g >= 2 lanes per ray; ws holds 32 rays + their results)
+static_assert(kGfRays * 10 * sizeof(float) <= kCoopWaveBytes, "coop scratch: 8 floats per ray + 2 result words");
+#ifndef RTX_GF_STEPS  // scan steps (2 spheres each) per resolve round: a 32-bit flag mask (stress build: 1)
+#define RTX_GF_STEPS 16
 #endif
-constexpr uint32_t kSmRays = 8, kSmCand = RTX_SM_CAND;
-static_assert((160 + kSmCand) * sizeof(float) <= kCoopWaveBytes, "sphere-major coop LDS");
-template <typename Q4>
-__device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *rad, uint64_t act, bool active,
-                                         f3 o, f3 d, float a, float inv_a, float t_min, float *ws, float &best,
-                                         bool &seq, unsigned long long *cp, unsigned long long *tq) {
+constexpr uint32_t kGfSteps = RTX_GF_STEPS;
+static_assert(kGfSteps >= 1 && kGfSteps <= 16, "flag mask: 2 bits per step in 32");
+template <typename Src>
+__device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src, uint64_t act, bool active, f3 o, f3 d,
+                                                float a, float inv_a, float t_min, float *ws, float &best, bool &seq,
+                                                unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m_all = (uint32_t)__popcll(act);
     const uint32_t rank_all =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-    float *rays = ws;        // [kSmRays][8]: o, d, a, inv_a
-    float *lines = ws + 64;  // [kSmRays][8]: LineTest
-    unsigned long long *keys = reinterpret_cast<unsigned long long *>(ws + 128);
-    uint32_t *bad = reinterpret_cast<uint32_t *>(ws + 144);
-    uint32_t *count = reinterpret_cast<uint32_t *>(ws + 152);
-    uint32_t *pairs = reinterpret_cast<uint32_t *>(ws + 160);
-    const LineTest T0 = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
-    const uint32_t n = S.n;
+    uint32_t *keys = reinterpret_cast<uint32_t *>(ws + 8 * kGfRays);  // [kGfRays][2]: the group results
     const float inf = __uint_as_float(0x7f800000u);
     int result = -1;
     seq = false;
 #pragma unroll 1
-    for (uint32_t c0 = 0; c0 < m_all; c0 += kSmRays) {
-        const uint32_t m = min(m_all - c0, kSmRays);
+    for (uint32_t c0 = 0; c0 < m_all; c0 += kGfRays) {
+        const uint32_t m = min(m_all - c0, kGfRays);
         const bool mine = active && rank_all >= c0 && rank_all < c0 + m;
         const uint32_t rank = rank_all - c0;
         if (mine) {
-            float *w = rays + 8 * rank;
+            float *w = ws + 8 * rank;
             w[0] = o.x;
             w[1] = o.y;
             w[2] = o.z;
@@ -781,113 +681,87 @@ __device__ __forceinline__ int groups_sm(const KScene &S, Q4 sph4, const float *
             w[5] = d.z;
             w[6] = a;
             w[7] = inv_a;
-            float *t = lines + 8 * rank;
-            t[0] = T0.ux;
-            t[1] = T0.uz;
-            t[2] = T0.vx;
-            t[3] = T0.vy;
-            t[4] = T0.vz;
-            t[5] = T0.nou;
-            t[6] = T0.nov;
-            t[7] = T0.thr;
-            keys[rank] = ~0ull;
-            bad[rank] = 0u;
         }
-        if (lane == 0u) *count = 0u;
         __builtin_amdgcn_wave_barrier();
         RTX_CP(0)
+        const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
+        const uint32_t g = 1u << lg;
+        const uint32_t r = lane >> lg, k = lane & (g - 1u);
+        const bool valid = r < m;
+        const float *w = ws + 8 * (valid ? r : 0u);
+        const f3 ro = mk3(w[0], w[1], w[2]), rd = mk3(w[3], w[4], w[5]);
+        const float ra = w[6], ria = w[7];
+        const LineTest T = line_test_setup(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ra, S.smag);
+        const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+        const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
+        uint64_t key = hit_key(inf, -1);
+        bool ok = true;
+        const uint32_t nsteps = valid ? (src.npairs + g - 1u) >> lg : 0u;
+        const uint32_t plast = src.npairs - 1u;
 #pragma unroll 1
-        for (uint32_t r = 0; r < m; r += 2u) {
-            // rays r and r + 1 (r again when m is odd), wave-uniform: in scalars
-            const uint32_t r1 = min(r + 1u, m - 1u);
-            const float *t0 = lines + 8 * r, *t1 = lines + 8 * r1;
-            auto rl2 = [&](int k) {
-                const f2v v = {read_lane(t0[k], 0), read_lane(t1[k], 0)};
-                return v;
+        for (uint32_t s0 = 0; __ballot(s0 < nsteps) != 0ull; s0 += kGfSteps) {
+            // scan: steps [s0, s1), pair p = st * g + k (spheres 2p, 2p + 1).
+            // The NOT-flagged bits are shifted in (q - thr >= +0 exactly when
+            // flagged, q finite): after the round, bit 2i + w of ~im is
+            // sphere 2p + w of step s1 - 1 - i.
+            uint32_t im = 0;
+            const uint32_t s1 = min(s0 + kGfSteps, nsteps);
+            auto step = [&](uint32_t st) {
+                f2v cx, cy, cz, R;
+                src.pair(Src::kPadded ? (st << lg) + k : min((st << lg) + k, plast), cx, cy, cz, R);
+                const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+                const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
+                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
+                im = (im << 1) | (__float_as_uint(q.y) >> 31);
+                im = (im << 1) | (__float_as_uint(q.x) >> 31);
             };
-            const f2v ux = rl2(0), uz = rl2(1), vx = rl2(2), vy = rl2(3), vz = rl2(4), nou = rl2(5), nov = rl2(6);
-            const float thr0 = read_lane(t0[7], 0), thr1 = read_lane(t1[7], 0);
-#pragma unroll 2
-            for (uint32_t j = lane; j < n; j += 64u) {
-                const float4 pq = sph4[j];
-                const f2v cx = {pq.x, pq.x}, cy = {pq.y, pq.y}, cz = {pq.z, pq.z}, R = {pq.w, pq.w};
-                // line_test_q's ops, per element
-                const f2v pu = fma2(cx, ux, fma2(cz, uz, nou));
-                const f2v pv = fma2(cx, vx, fma2(cy, vy, fma2(cz, vz, nov)));
-                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R));
-                if (!(q.x < thr0)) {
-                    const uint32_t k = atomicAdd(count, 1u);
-                    if (k < kSmCand) pairs[k] = (j << 3) | r;
-                }
-                if (r1 != r && !(q.y < thr1)) {
-                    const uint32_t k = atomicAdd(count, 1u);
-                    if (k < kSmCand) pairs[k] = (j << 3) | r1;
-                }
+            uint32_t st = s0;
+            for (; st + 2u <= s1; st += 2u) {
+                step(st);
+                step(st + 1u);
+            }
+            if (st < s1) step(st);
+            const uint32_t nb = 2u * (s1 > s0 ? s1 - s0 : 0u);
+            uint32_t fm = ~im & (nb >= 32u ? ~0u : ((1u << nb) - 1u));
+            // resolve this round's flags, one sphere per lane per iteration
+#pragma unroll 1
+            while (__ballot(fm != 0u) != 0ull) {
+                const bool live = fm != 0u;
+                const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
+                fm &= fm - 1u;
+                const uint32_t p = ((s1 - 1u - (bit >> 1)) << lg) + k;
+                const uint32_t j = 2u * (Src::kPadded ? p : min(p, plast)) + (bit & 1u);
+                resolve_one(src.sphere(j), (int)j, live, ro, rd, ra, ria, t_min, key, ok);
             }
         }
-        __builtin_amdgcn_wave_barrier();
         RTX_CP(1)
-        const uint32_t K = *count;
-#pragma unroll 1
-        for (uint32_t k = lane; k < min(K, kSmCand); k += 64u) {
-            const uint32_t e = pairs[k];
-            const uint32_t j = e >> 3, r = e & 7u;
-            const float *w = rays + 8 * r;
-            const float4 pq = sph4[j];
-            const float rr = rad ? rad[j] : S.cen[j].w;
-            // resolve_one's ops for one candidate
-            const float ocx = w[0] - pq.x;
-            const float ocy = w[1] - pq.y;
-            const float ocz = w[2] - pq.z;
-            const float hb = fmaf(ocz, w[5], fmaf(ocy, w[4], ocx * w[3]));
-            const float cc = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -(rr * rr))));
-            const float disc = fmaf(hb, hb, -(w[6] * cc));
-            if (disc < 0.0f) continue;
-            const float sq = sqrt_rn(disc);
-            const float rn = (-hb - sq) * w[7];
-            const float rf = (-hb + sq) * w[7];
-            if (!(fabsf(rn) < inf && fabsf(rf) < inf)) {
-                atomicOr(&bad[r], 1u);
-                continue;
-            }
-            const bool use_n = !(rn < t_min);
-            const float c = use_n ? rn : rf;
-            if (use_n || !(rf < t_min))  // c >= t_min > 0: its bits order like its value
-                atomicMin(&keys[r], ((unsigned long long)__float_as_uint(c) << 32) | (unsigned long long)(0xffffffffu - j));
+        // the group's (min c, then the largest index among equal c)
+        const uint32_t cb0 = (uint32_t)(key >> 32);
+        const uint32_t cb = group_reduce_u32<false>(cb0, lg);
+        const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? ~(uint32_t)key : 0u, lg);  // index + 1, 0: none
+        const uint64_t badm = __ballot(!ok);
+        if (valid && k == 0u) {
+            const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
+            keys[2 * r] = (badm & gm) != 0ull ? 0xffffffffu : ib;  // ~0: a non-finite root in the group
+            keys[2 * r + 1] = cb;
         }
         __builtin_amdgcn_wave_barrier();
         RTX_CP(2)
         if (mine) {
-            if (K > kSmCand || bad[rank] != 0u) {
+            const uint32_t kb = keys[2 * rank], kc = keys[2 * rank + 1];
+            if (kb == 0xffffffffu) {
                 seq = true;
-            } else {
-                const unsigned long long kk = keys[rank];
-                const float c = __uint_as_float((uint32_t)(kk >> 32));
-                if (kk != ~0ull && c <= best) {  // accepted iff c <= t_max
+            } else if (kb != 0u) {
+                const float c = __uint_as_float(kc);
+                if (c <= best) {  // accepted iff c <= t_max
                     best = c;
-                    result = (int)(0xffffffffu - (uint32_t)kk);
+                    result = (int)(kb - 1u);
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();  // the next chunk reuses the LDS
     }
     return active ? result : -1;
-}
-
-#undef RTX_CP
-
-template <typename Q4>
-__device__ __forceinline__ int hit_world_groups(const KScene &S, Q4 sph4, const float *rad, uint64_t act,
-                                                bool active, f3 o, f3 d, float a, float inv_a, float t_min,
-                                                float *ws, uint32_t *list, float &best, bool &seq,
-                                                unsigned long long *cp = nullptr, unsigned long long *tq = nullptr) {
-    if (__popcll(act) == 1)
-        return groups_impl<true>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
-    // 2-3 rays: groups of 32 or 16 lanes scan short chunks; from 4 rays on
-    // (chunks of 31+ spheres per lane) the sphere-major pass is faster
-    if (__popcll(act) >= kCoopSm)
-        return groups_sm(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, best, seq, cp, tq);
-    return groups_impl<false>(S, sph4, rad, act, active, o, d, a, inv_a, t_min, ws, list, best, seq, cp, tq);
 }
 
 // Lane state: the pixel it is tracing and that pixel's current path.
@@ -1072,9 +946,7 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
         if (L.sample >= P.spp) {
             write_pixel<kCost>(P, L);
             L.active = false;
-#if RTX_DIAG_PIXEL
-            if (P.wave_times && L.gid < P.wave_cap) P.wave_times[2 * L.gid + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
+            diag_pixel_end(P, L.gid);
         } else {
             begin_sample(P, F, L.x, L.y, L);
         }
@@ -1148,9 +1020,7 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
         if (g < hi) {
             start_pixel(P, F, P.perm ? P.perm[g] : g, L);
             L.slot = g;
-#if RTX_DIAG_PIXEL
-            if (P.wave_times && L.gid < P.wave_cap) P.wave_times[2 * L.gid] = __builtin_amdgcn_s_memrealtime() << 2;
-#endif
+            diag_pixel_start(P, L.gid, 0);
         }
     }
     return base + cnt >= hi;
@@ -1185,10 +1055,7 @@ __device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint
     const uint32_t rk = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
     if (!L.active && rk < take) {
         start_pixel(P, F, P.perm[h + rk], L);
-#if RTX_DIAG_PIXEL
-        if (P.wave_times && L.gid < P.wave_cap)
-            P.wave_times[2 * L.gid] = (__builtin_amdgcn_s_memrealtime() << 2) | (ctr == P.heavy ? 1ull : 2ull);
-#endif
+        diag_pixel_start(P, L.gid, ctr == P.heavy ? 1ull : 2ull);
     }
     if (h + room >= hi) done = true;
     return true;
@@ -1220,17 +1087,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     constexpr uint32_t kLB = list_bytes<kPF>();
     float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
     (void)coop_ws;
-    // the coop's sphere data: a block-wide LDS copy of pre4 for small scenes
-    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes);
-    float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
+    // the coop's sphere data: a block-wide LDS copy for small scenes (SphLds)
     const bool coop_lds = P.scene.n <= kCoopLds;
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds);
+    const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
     if (coop_lds) {
-        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
-            s_pre4[i] = P.scene.pre4[i];
-            s_rad[i] = P.scene.cen[i].w;
-        }
         __syncthreads();
     } else if (kPF) {
         if (threadIdx.x == 0) *pack = 0u;
@@ -1257,45 +1120,19 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
-#if RTX_DIAG_PROF
-    // [0] refill clocks [1] hit_world [2] shade [3] tail mode [4] iterations [5] tail iterations
-    // [6] active lanes summed over iterations
-    unsigned long long pr[7] = {0, 0, 0, 0, 0, 0, 0};
-    if ((threadIdx.x & 63u) == 0u)
-        for (int k = 0; k < 8; ++k) diag_slots()[k] = 0u;
-    unsigned long long tq = __builtin_readcyclecounter();
-#define RTX_PROF(k)                                          \
-    {                                                        \
-        const unsigned long long tn = __builtin_readcyclecounter(); \
-        pr[k] += tn - tq;                                    \
-        tq = tn;                                             \
-    }
-#else
-#define RTX_PROF(k)
-#endif
-#if RTX_DIAG_COOP
-    // tier-1 coop segments: [0] ray exchange + line setup [1] scan + resolve
-    // [2] reduction [3] shade [4] loop overhead [5] segments
-    unsigned long long cpa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long ctq = __builtin_readcyclecounter();
-    bool was_t1 = false;
-#endif
+    Diag D;
+    D.begin();
     for (;;) {
         if (!(H.t1_done && H.t2_done) && (H.tier != 0u || __ballot(L.active) == 0ull)) take_heavy(P, F, H, L);
         if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
         const bool heavy = H.tier != 0u;
         if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
         const uint64_t act = __ballot(L.active);
-        RTX_PROF(0)
+        D.section(0);
         if (act == 0ull) break;  // spp, depth > 0: idle after both queues => drained
-#if RTX_DIAG_PROF
-        pr[4]++;
-        pr[6] += __popcll(act);
-#endif
+        D.iteration(act);
         if (heavy || (exhausted && (uint32_t)__popcll(act) <= P.coop_max)) {
-#if RTX_DIAG_PROF
-            pr[5]++;
-#endif
+            D.tail_iteration();
             // Frame tail: the few pixels left in this wave are its critical
             // path; trace their rays together, several lanes per ray.
             float my_best = __uint_as_float(0x7f800000u);
@@ -1307,24 +1144,12 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(kTailPrio);
-#if RTX_DIAG_COOP
-            unsigned long long *cp = H.tier == (uint32_t)RTX_DIAG_COOP ? cpa : nullptr;
-            unsigned long long *ctqp = &ctq;
-            if (H.tier == (uint32_t)RTX_DIAG_COOP) {
-                const unsigned long long tn = __builtin_readcyclecounter();
-                if (was_t1) cpa[4] += tn - ctq;
-                ctq = tn;
-                cpa[5]++;
-            }
-#else
-            unsigned long long *cp = nullptr, *ctqp = nullptr;
-#endif
-            int my_hit = coop_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, (const float *)s_rad, act,
-                                                     L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list,
-                                                     my_best, my_seq, cp, ctqp)
-                                  : hit_world_groups(P.scene, P.scene.pre4, (const float *)nullptr, act, L.active,
-                                                     L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list, my_best, my_seq,
-                                                     cp, ctqp);
+            unsigned long long *ctqp;
+            unsigned long long *cp = D.coop_begin(H.tier, ctqp);
+            int my_hit = coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
+                                                     coop_ws, my_best, my_seq, cp, ctqp)
+                                  : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
+                                                     coop_ws, my_best, my_seq, cp, ctqp);
             if (L.active) {
                 if (my_seq) {
                     my_best = __uint_as_float(0x7f800000u);
@@ -1332,16 +1157,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 }
                 shade<kCost>(P, F, L, min(my_hit, last), my_best);
             }
-#if RTX_DIAG_COOP
-            if (cp) {
-                const unsigned long long tn = __builtin_readcyclecounter();
-                cpa[3] += tn - ctq;
-                ctq = tn;
-            }
-            was_t1 = H.tier == (uint32_t)RTX_DIAG_COOP;
-#endif
+            D.coop_end(cp, H.tier);
             if (H.tier == 0u) __builtin_amdgcn_s_setprio(0);  // a heavy wave keeps its priority
-            RTX_PROF(3)
+            D.section(3);
             continue;
         }
         // lane mode: a wave that holds one of the heaviest pixels of the
@@ -1354,32 +1172,20 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
-            // from it (same centre floats, cen.w = s_rad) instead of HBM/L2
+            // from it (the same centre and radius floats as cen) instead of HBM/L2
             const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
-                                ? hit_world_pre_ld<kPF>(P.scene,
-                                                        [s_pre4, s_rad](uint32_t i) {
-                                                            const float4 c = s_pre4[i];
-                                                            return make_float4(c.x, c.y, c.z, s_rad[i]);
-                                                        },
-                                                        L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                                ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
+                                                        L.a, L.inv_a, kTMin, best, list, nullptr, 0,
+                                                        RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
-            RTX_PROF(1)
+            D.section(1);
             shade<kCost>(P, F, L, min(hit, last), best);
         }
-        RTX_PROF(2)
+        D.section(2);
     }
-#if RTX_DIAG_PROF
-    if (P.wave_times && (threadIdx.x & 63u) == 0u)
-        for (int k = 0; k < 7; ++k) atomicAdd(&P.wave_times[k], pr[k]);
-    if (P.wave_times && (threadIdx.x & 63u) == 0u)
-        for (int k = 0; k < 5; ++k) atomicAdd(&P.wave_times[8 + k], (unsigned long long)diag_slots()[k]);
-#endif
-#if RTX_DIAG_COOP
-    if (P.wave_times && (threadIdx.x & 63u) == 0u)
-        for (int k = 0; k < 6; ++k) atomicAdd(&P.wave_times[k], cpa[k]);
-#endif
+    D.finish(P);
     count_segments(P, L.segs);
-    if (!RTX_DIAG_PROF && !RTX_DIAG_PIXEL && !RTX_DIAG_COOP && P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only
+    if (!kDiagAny && P.wave_times && (threadIdx.x & 63u) == 0u) {  // diagnostic only (rtx_debug_wave_times)
         const uint32_t w = blockIdx.x * (kRB / 64) + threadIdx.x / 64;
         P.wave_times[2 * w] = t_start;
         P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1464,44 +1270,35 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
 
 // Heavy-pixel split: with key k ~ a pixel's cost, a lane's share of the
 // frame is W / lanes (W = sum of keys). Pixels whose key exceeds
-// kHeavy1Alpha times it form tier 1 (slots [0, k1): one pixel per wave,
-// 64 lanes per ray). When there are fewer pixels than kHeavyRho per
+// a1 times it form tier 1 (slots [0, k1): one pixel per wave,
+// 64 lanes per ray). When there are fewer pixels than rho per
 // resident lane (a small share of a frame, e.g. one GPU's rows of an 8-GPU
-// split), the tier-1 bar rises to kHeavy1AlphaSmall times the share
-// and the pixels above kHeavyAlpha times it (up to that bar) form tier
-// 2 (slots [k1, kh), kHeavy2 per wave). Tiers and alphas were chosen with
-// tools/part_scaling.py on C2 split 1/2/4/8 ways. Writes kh to heavy[1] and
+// split), the tier-1 bar rises to a1_small times the share
+// and the pixels above a2_small times it (up to that bar) form tier
+// 2 (slots [k1, kh), kHeavy2 per wave). Tiers and bars were chosen with
+// tools/part_scaling.py on C2 split 1/2/4/8 ways (the defaults below);
+// rtx_set_schedule (include/rtx.h) replaces them per context, and
+// tools/heavy_sweep.py sweeps them through it. Writes kh to heavy[1] and
 // k1 to heavy[3]. One thread: 256 buckets.
-// The split's bars; tools/heavy_sweep.py overrides them
-// through RTX_HEAVY (host side, launch_render) to tune them on the box.
-struct HeavyTune {
-    double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
-    double occ_small, occ_low, occ_normal;  // fraction of the resident waves launched for a small / low / larger share
-    double coop_max;            // KParams::coop_max
-};
-static HeavyTune heavy_tune() {
-    HeavyTune t{kHeavy1Alpha, kHeavy1AlphaSmall, kHeavy1AlphaLow, kHeavyAlpha, kHeavy2AlphaMedium,
-                kHeavyRho,   kHeavyRhoLow,      kHeavyRho2,      kPrioFracX100 / 100.0,
-                1.0,         1.0,               1.0,               (double)kCoopMax};
-    const char *e = getenv("RTX_HEAVY");  // "a1=1.7,a2s=2,..." (diagnostic tuning only)
-    if (!e) return t;
-    const struct { const char *k; double *v; } keys[] = {
-        {"a1", &t.a1},   {"a1s", &t.a1_small}, {"a1l", &t.a1_low},   {"a2s", &t.a2_small}, {"a2m", &t.a2_medium},
-        {"rho", &t.rho}, {"rhol", &t.rho_low}, {"rho2", &t.rho2},    {"prio", &t.prio_frac},
-        {"occs", &t.occ_small}, {"occl", &t.occ_low}, {"occn", &t.occ_normal}, {"coop", &t.coop_max}};
-    for (const char *q = e; *q;) {
-        const char *eq = strchr(q, '=');
-        if (!eq) break;
-        for (const auto &k : keys)
-            if (strlen(k.k) == (size_t)(eq - q) && strncmp(q, k.k, eq - q) == 0) *k.v = atof(eq + 1);
-        const char *c = strchr(eq, ',');
-        if (!c) break;
-        q = c + 1;
-    }
+}  // namespace
+KTune default_tune() {
+    KTune t;
+    t.a1 = kHeavy1Alpha;
+    t.a1_small = kHeavy1AlphaSmall;
+    t.a1_low = kHeavy1AlphaLow;
+    t.a2_small = kHeavyAlpha;
+    t.a2_medium = kHeavy2AlphaMedium;
+    t.rho = kHeavyRho;
+    t.rho_low = kHeavyRhoLow;
+    t.rho2 = kHeavyRho2;
+    t.prio_frac = kPrioFracX100 / 100.0;
+    t.occ_small = t.occ_low = t.occ_normal = 1.0;
+    t.coop_max = (uint32_t)kCoopMax;
     return t;
 }
+namespace {
 __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t *heavy,
-                              const HeavyTune t) {
+                              const KTune t) {
     if (threadIdx.x != 0u) return;
     double w = 0.0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) w += (double)counts[b] * (double)(kCostBuckets - 1u - b);
@@ -1616,17 +1413,11 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
     float *coop_ws = reinterpret_cast<float *>(s_mem + kLB) + (threadIdx.x / 64) * (kCoopWaveBytes / 4);
     // this wave's batch slots: [k][0 px0, 1 npx, 2 items (0 = free), 3 items done]
     uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
-    float4 *s_pre4 = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes + kPsStateBytes);
-    float *s_rad = reinterpret_cast<float *>(s_pre4 + P.scene.n);
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
+    const SphGlobal sg = sph_global(P.scene);
     const uint32_t lane = threadIdx.x & 63u;
     if (lane < kPsSlots * 4) st[lane] = 0u;
-    if (sph_lds) {
-        for (uint32_t i = threadIdx.x; i < P.scene.n; i += kRB) {
-            s_pre4[i] = P.scene.pre4[i];
-            s_rad[i] = P.scene.cen[i].w;
-        }
-    }
     __syncthreads();
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
@@ -1684,21 +1475,17 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
         if (exhausted && __popcll(act) <= kCoopMax) {  // the wave's last few samples: group coop
             __builtin_amdgcn_s_setprio(kTailPrio);
             bool seq = false;
-            hit = sph_lds ? hit_world_groups(P.scene, (const float4 *)s_pre4, (const float *)s_rad, act, L.active,
-                                             L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, list, best, seq)
-                          : hit_world_groups(P.scene, P.scene.pre4, (const float *)nullptr, act, L.active, L.o, L.d,
-                                             L.a, L.inv_a, kTMin, coop_ws, list, best, seq);
+            hit = sph_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
+                                             seq)
+                          : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
+                                             seq);
             if (L.active && seq) {  // a non-finite root in the group: the exact path
                 best = __uint_as_float(0x7f800000u);
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {
-            hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene,
-                                                  [s_pre4, s_rad](uint32_t i) {
-                                                      const float4 c = s_pre4[i];
-                                                      return make_float4(c.x, c.y, c.z, s_rad[i]);
-                                                  },
-                                                  L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+            hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
+                                                  L.inv_a, kTMin, best, list)
                           : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
         }
         if (L.active) {
@@ -1763,9 +1550,11 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
     img[i] = g[((uint64_t)part * max_rows + lr) * width + x];
 }
 
+// t_min > 0 and t_max >= t_min (rtx_debug_hit_world checks): the resolve
+// orders roots by their bits (hit_key).
 __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const float *rays,
                                                             uint32_t nrays, float t_min,
-                                                            float t_max, float *out) {
+                                                            float t_max, uint32_t start, float *out) {
     __shared__ uint32_t list[list_bytes<true>() > kListBytes ? list_bytes<true>() / sizeof(uint32_t)
                                                              : kListBytes / sizeof(uint32_t)];
     const uint32_t i = blockIdx.x * kRB + threadIdx.x;
@@ -1775,9 +1564,10 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     const float a = dir_len2(d);
     const float inv_a = 1.0f / a;
     float best = t_max;
-    const int idx = min((S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list)
-                                                             : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list)),
-                        (int)S.n - 1);
+    const int idx =
+        min((S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
+                                  : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)),
+            (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
         for (int k = 0; k < 10; ++k) r[k] = 0.0f;
@@ -1892,7 +1682,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() + 16 : kListBytes) + kCoopBytes +  // kPF: the pack word
-           (s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
+           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
@@ -1918,7 +1708,7 @@ constexpr uint32_t kPsItems = RTX_PS_ITEMS;
 constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
-           (!use_pf(s) && s.n <= kCoopLds ? (size_t)s.n * (sizeof(float4) + sizeof(float)) : 0);
+           (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }
 static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
@@ -1960,9 +1750,9 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
 }
 
 hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
-    const HeavyTune tune = heavy_tune();
+    const KTune &tune = sched.tune;  // validated by rtx_set_schedule
     KParams p = p_in;
-    p.coop_max = (uint32_t)min(max(tune.coop_max, 1.0), 64.0);
+    p.coop_max = min(max(tune.coop_max, 1u), 64u);
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t need = ceil_div(lanes, kRB);
@@ -2048,10 +1838,10 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
 }
 
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays, float t_min,
-                                  float t_max, float *out, hipStream_t stream) {
+                                  float t_max, uint32_t start_block, float *out, hipStream_t stream) {
     if (nrays == 0) return hipSuccess;
     hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
-                       rays, nrays, t_min, t_max, out);
+                       rays, nrays, t_min, t_max, start_block, out);
     return hipGetLastError();
 }
 

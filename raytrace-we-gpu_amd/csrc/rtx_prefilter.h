@@ -8,31 +8,38 @@
 // ray's LINE. The kernel's scan does not evaluate the reference's disc
 // (11 fp32 ops per sphere); it evaluates
 //     Q = R_i - (c.u - o.u)^2 - (c.v - o.v)^2          (7 fp32 ops)
-// with (u, v) an orthonormal basis of the plane perpendicular to d, u
-// chosen with u.y = 0 so that c.u needs two fma instead of three, and flags
-// the sphere as a candidate when Q >= thr. R_i = r^2 + margin(c, r) and
-// thr = -margin(o) are inflated so that
+// with (u, v) an orthonormal basis of the plane perpendicular to d, v
+// chosen with v.x = 0 (v = (0, dz, -dy) / |(dy, dz)|, u = d/|d| x v), and
+// flags the sphere as a candidate when Q >= thr. R_i = r^2 + margin(c, r)
+// and thr = -margin(o) are inflated so that
 //     reference disc >= 0 (or NaN)  ==>  Q >= thr,
 // i.e. the prefilter never drops a sphere the reference would test further.
 // A flagged sphere is resolved with the reference's own op sequence
-// (rtx_kernels.hip, resolve_candidates), which rejects false positives, so
-// the scan's answer is bit-identical to the reference's.
+// (rtx_kernels.hip, resolve_one), which rejects false positives, so the
+// scan's answer is bit-identical to the reference's.
+// Why v.x = 0: on a "flat" block (all 8 centres at one height cy, as every
+// small sphere of the RTIOW scenes at y = 0.2) the cy terms of both
+// projections are per-ray constants, so c.u - o.u is 2 fma (cx, cz) and
+// c.v - o.v ONE fma (cz only): 5 fp32 ops per test instead of 6 with the
+// round-2 basis (u.y = 0), whose two projections both kept cx and cz.
 //
-// Error bound (u = unit roundoff 2^-24, S = |c| + |o|):
+// Error bound (u = unit roundoff 2^-24, S = |c| + |o|). The
+// basis is the round-2 one with the x and y axes exchanged, so the
+// term-by-term bound is the same:
 //   reference disc rounding, divided by a:    13|oc|^2 + 7r^2
 //   oc = fl(o - c) perturbation:               2|oc|^2
-//   basis (u, v) error (<= 4u, 10u per vector): 23|oc|^2
-//   c.u - o.u, c.v - o.v chains (4u S, 6u S):  15 S^2
+//   basis (u, v) error (<= 10u, 4u per vector): 23|oc|^2
+//   c.u - o.u, c.v - o.v chains (6u S, 4u S):  15 S^2
 //   final two fma:                              4r^2
 //   total <= u (53 S^2 + 11 r^2) <= u (106|c|^2 + 106|o|^2 + 11 r^2)
 // The basis is built with the 1-ulp hardware reciprocal square root
-// (v_rsq_f32: 1/|(dx, dz)| and 1/|d|), not IEEE sqrt and division: it only
+// (v_rsq_f32: 1/|(dy, dz)| and 1/|d|), not IEEE sqrt and division: it only
 // has to be close to orthonormal, its error is in the bound above, and it
 // saves ~55 VALU instructions per ray segment.
 // The margins below are 1.6e-5 (= 268u) per |c|^2 and |o|^2 and 2e-6
 // (= 33u) per r^2, i.e. >= 2.5x that bound, plus an absolute 1e-24 that
 // covers subnormal rounding in the region the per-lane `safe` test admits
-// (a in [2^-40, 2^40], ray not within ~2^-20 rad of vertical, no fp32
+// (a in [2^-40, 2^40], ray not within ~2^-20 rad of the x axis, no fp32
 // overflow). Lanes outside that region get u = v = 0 and thr = -inf: every
 // sphere is flagged and the lane ends on the exact sequential path.
 #pragma once
@@ -54,8 +61,8 @@ constexpr double kPreMarginR = 2e-6;    // per r^2   (sphere side, R_i)
 constexpr float kPreFloor = 1e-24f;
 
 struct LineTest {
-    float ux, uz;      // u = (-dz, 0, dx) / |(dx, dz)|
-    float vx, vy, vz;  // v = d/|d| x u
+    float ux, uy, uz;  // u = d/|d| x v = (-(dy^2 + dz^2), dx*dy, dx*dz) / (|d| |(dy, dz)|)
+    float vy, vz;      // v = (0, dz, -dy) / |(dy, dz)|   (v.x = 0)
     float nou, nov;    // -(o.u), -(o.v)
     float thr;         // flag the sphere when Q >= thr
 };
@@ -91,34 +98,34 @@ inline float pf_sqrt(float x) { return pf_nudge((float)sqrt((double)x), pf_host_
 RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy, float dz, float a,
                                 float smag) {
     LineTest T;
-    const float n2 = fmaf(dx, dx, dz * dz);
+    const float m2 = fmaf(dy, dy, dz * dz);
     const float o2 = fmaf(ox, ox, fmaf(oy, oy, oz * oz));
-    // a in [2^-40, 2^40]; d not within ~2^-20 rad of the y axis; S = smag +
+    // a in [2^-40, 2^40]; d not within ~2^-20 rad of the x axis; S = smag +
     // |o| with S^2 and a*S^2 <= 1e36 (no fp32 overflow in disc or Q).
     // NaN or infinite inputs fail these tests.
     const float so = smag + pf_sqrt(o2);  // only bounds the magnitudes (1e36 vs fp32's 3.4e38)
     const float so2 = so * so;
-    const bool safe = a >= 9.094947e-13f && a <= 1.0995116e12f && n2 >= a * 9.094947e-13f &&
+    const bool safe = a >= 9.094947e-13f && a <= 1.0995116e12f && m2 >= a * 9.094947e-13f &&
                       so2 <= 1e36f && a * so2 <= 1e36f;
     if (!safe) {
-        T.ux = T.uz = T.vx = T.vy = T.vz = T.nou = T.nov = 0.0f;
+        T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
         T.thr = -INFINITY;
         return T;
     }
 #if defined(__HIP_DEVICE_COMPILE__)
-    const float inv_n = pf_rsq(n2);  // n2 >= 2^-80 and a >= 2^-40 here: normal inputs
-    const float w = pf_rsq(a) * inv_n;
+    const float inv_m = pf_rsq(m2);  // m2 >= 2^-80 and a >= 2^-40 here: normal inputs
+    const float w = pf_rsq(a) * inv_m;
 #else
-    const float inv_n = pf_rsq_k(n2, 0);
-    const float w = pf_rsq_k(a, 1) * inv_n;
+    const float inv_m = pf_rsq_k(m2, 0);
+    const float w = pf_rsq_k(a, 1) * inv_m;
 #endif
-    T.ux = -dz * inv_n;
-    T.uz = dx * inv_n;
-    T.vx = (dx * dy) * w;
-    T.vy = -(n2 * w);
-    T.vz = (dy * dz) * w;
-    T.nou = -fmaf(oz, T.uz, ox * T.ux);
-    T.nov = -fmaf(oz, T.vz, fmaf(oy, T.vy, ox * T.vx));
+    T.vy = dz * inv_m;
+    T.vz = -dy * inv_m;
+    T.ux = -(m2 * w);
+    T.uy = (dx * dy) * w;
+    T.uz = (dx * dz) * w;
+    T.nou = -fmaf(oz, T.uz, fmaf(oy, T.uy, ox * T.ux));
+    T.nov = -fmaf(oz, T.vz, oy * T.vy);
     T.thr = -fmaf(o2, kPreMarginO, kPreFloor);
     return T;
 }
@@ -126,22 +133,30 @@ RTX_HD LineTest line_test_setup(float ox, float oy, float oz, float dx, float dy
 // Q for one sphere; the kernel runs the same op sequence on sphere pairs
 // (v_pk_fma_f32), i.e. the same IEEE fma per element.
 RTX_HD float line_test_q(const LineTest &T, float cx, float cy, float cz, float R) {
-    const float pu = fmaf(cx, T.ux, fmaf(cz, T.uz, T.nou));
-    const float pv = fmaf(cx, T.vx, fmaf(cy, T.vy, fmaf(cz, T.vz, T.nov)));
+    const float pu = fmaf(cx, T.ux, fmaf(cy, T.uy, fmaf(cz, T.uz, T.nou)));
+    const float pv = fmaf(cy, T.vy, fmaf(cz, T.vz, T.nov));
     return fmaf(-pv, pv, fmaf(-pu, pu, R));
 }
 
-// Flat blocks: all 8 spheres of a block share one centre height cy (the
-// RTIOW scenes' small spheres all sit at y = 0.2). The cy term of c.v is
-// then one per-ray value, kv = fl(cy*vy - o.v), computed once per segment,
-// and a test costs 6 fp32 ops instead of 7. c.v - o.v is still a chain of
-// three fma over the same four terms (cy*vy first instead of second), so
-// the rounding bound of that chain (6u S) and the margins above are
-// unchanged; tests/prefilter_check.cpp checks both orders.
-RTX_HD float line_test_kv(const LineTest &T, float cy) { return fmaf(cy, T.vy, T.nov); }
-RTX_HD float line_test_q_flat(const LineTest &T, float kv, float cx, float cz, float R) {
-    const float pu = fmaf(cx, T.ux, fmaf(cz, T.uz, T.nou));
-    const float pv = fmaf(cx, T.vx, fmaf(cz, T.vz, kv));
+// Flat blocks: all 8 spheres of a block share one centre height cy. The cy
+// terms of c.u and c.v are then per-ray values, ku = fl(cy*uy - o.u) and
+// kv = fl(cy*vy - o.v), computed once per segment, and a test costs 5 fp32
+// ops (c.u: 2 fma, c.v: 1 fma, Q: 2 fma) instead of 7. Both projections are
+// still fma chains over the same terms (cy first instead of second), so the
+// chains' rounding bounds (6u S, 4u S) and the margins above are unchanged;
+// tests/prefilter_check.cpp checks both orders.
+struct LineFlat {
+    float ku, kv;
+};
+RTX_HD LineFlat line_test_flat(const LineTest &T, float cy) {
+    LineFlat K;
+    K.ku = fmaf(cy, T.uy, T.nou);
+    K.kv = fmaf(cy, T.vy, T.nov);
+    return K;
+}
+RTX_HD float line_test_q_flat(const LineTest &T, const LineFlat &K, float cx, float cz, float R) {
+    const float pu = fmaf(cx, T.ux, fmaf(cz, T.uz, K.ku));
+    const float pv = fmaf(cz, T.vz, K.kv);
     return fmaf(-pv, pv, fmaf(-pu, pu, R));
 }
 

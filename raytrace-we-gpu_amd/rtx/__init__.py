@@ -52,6 +52,18 @@ class rtx_frame(C.Structure):
                 ("lens_u", C.c_float * 4), ("lens_v", C.c_float * 4)]
 
 
+class rtx_schedule(C.Structure):
+    """The chain render's schedule (include/rtx.h rtx_schedule)."""
+    _fields_ = [("tier1_bar", C.c_float), ("tier1_bar_small", C.c_float), ("tier1_bar_low", C.c_float),
+                ("tier2_bar_small", C.c_float), ("tier2_bar_medium", C.c_float), ("small_share", C.c_float),
+                ("low_share", C.c_float), ("medium_share", C.c_float), ("hot_fraction", C.c_float),
+                ("occupancy_small", C.c_float), ("occupancy_low", C.c_float), ("occupancy_normal", C.c_float),
+                ("tail_coop_max", C.c_uint32), ("reserved", C.c_uint32)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
 class rtx_stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_uint64), ("samples", C.c_uint64),
                 ("segments", C.c_uint64), ("sphere_tests", C.c_uint64)]
@@ -106,12 +118,21 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_camera_simple": (C.c_int, [u32, u32, C.POINTER(rtx_frame)]),
         "rtx_world_from_worlddef": (C.c_int, [vp, C.c_size_t, f, f, f, C.POINTER(rtx_world)]),
         "rtx_frame_from_perframe": (C.c_int, [vp, C.c_size_t, u32, u32, C.POINTER(rtx_frame)]),
+        "rtx_schedule_defaults": (C.c_int, [C.POINTER(rtx_schedule)]),
+        "rtx_set_schedule": (C.c_int, [ctx, C.POINTER(rtx_schedule)]),
+        "rtx_get_schedule": (C.c_int, [ctx, C.POINTER(rtx_schedule)]),
         "rtx_debug_hit_world": (C.c_int, [ctx, f, u32, C.c_float, C.c_float, f]),
+        "rtx_debug_hit_world_from": (C.c_int, [ctx, f, u32, C.c_float, C.c_float, u32, f]),
         "rtx_debug_math": (C.c_int, [ctx, C.c_int, f, f, u32, f]),
         "rtx_debug_wave_times": (C.c_int, [ctx, C.c_size_t, C.POINTER(C.c_uint64)]),
         "rtx_debug_pixel_cost": (C.c_int, [ctx, u32, C.POINTER(C.c_uint32)]),
     }
+    # entry points added after 1.0 may be absent from older builds (A/B runs
+    # of earlier libraries); calling one then fails with AttributeError
+    optional = {"rtx_schedule_defaults", "rtx_set_schedule", "rtx_get_schedule", "rtx_debug_hit_world_from"}
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -231,6 +252,13 @@ def part_row_ids(height: int, tile_rows: int, part: int, nparts: int) -> np.ndar
     return y[(y // tile_rows) % nparts == part].astype(np.uint32)
 
 
+def schedule_defaults() -> rtx_schedule:
+    """The library's default schedule (no GPU)."""
+    sch = rtx_schedule()
+    _check(load_library().rtx_schedule_defaults(C.byref(sch)), "rtx_schedule_defaults")
+    return sch
+
+
 def device_count() -> int:
     n = C.c_int(0)
     rc = load_library().rtx_device_count(C.byref(n))
@@ -334,12 +362,37 @@ class Context:
         _check(self._lib.rtx_get_stats(self._h, C.byref(s)), "rtx_get_stats")
         return s
 
+    def set_schedule(self, schedule: Optional[rtx_schedule] = None, **fields):
+        """Install a schedule (rtx_set_schedule): `schedule`, or the current
+        one with `fields` replaced; no arguments = the defaults."""
+        if schedule is None and not fields:
+            _check(self._lib.rtx_set_schedule(self._h, None), "rtx_set_schedule", self._lib)
+            return
+        sch = schedule if schedule is not None else self.get_schedule()
+        for k, v in fields.items():
+            if k not in dict(rtx_schedule._fields_):
+                raise RtxError(f"unknown schedule field {k}")
+            setattr(sch, k, v)
+        _check(self._lib.rtx_set_schedule(self._h, C.byref(sch)), "rtx_set_schedule", self._lib)
+
+    def get_schedule(self) -> rtx_schedule:
+        sch = rtx_schedule()
+        _check(self._lib.rtx_get_schedule(self._h, C.byref(sch)), "rtx_get_schedule", self._lib)
+        return sch
+
     def debug_hit_world(self, rays: np.ndarray, t_min: float = 0.001,
-                        t_max: float = float("inf")) -> np.ndarray:
+                        t_max: float = float("inf"), start_block: Optional[int] = None) -> np.ndarray:
+        """hit_world on the GPU (rtx_debug_hit_world); start_block: the scan
+        starts at that 8-sphere block and wraps round (rtx_debug_hit_world_from)."""
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
         out = np.zeros((rays.shape[0], 10), np.float32)
-        _check(self._lib.rtx_debug_hit_world(self._h, _fptr(rays), rays.shape[0], t_min, t_max,
-                                             _fptr(out)), "rtx_debug_hit_world")
+        if start_block is None:
+            _check(self._lib.rtx_debug_hit_world(self._h, _fptr(rays), rays.shape[0], t_min, t_max,
+                                                 _fptr(out)), "rtx_debug_hit_world", self._lib)
+        else:
+            _check(self._lib.rtx_debug_hit_world_from(self._h, _fptr(rays), rays.shape[0], t_min, t_max,
+                                                      start_block, _fptr(out)), "rtx_debug_hit_world_from",
+                   self._lib)
         return out
 
     def arm_wave_times(self, max_waves: int):

@@ -16,12 +16,13 @@ def lambert_cases(n=4000, seed=5):
     return np.concatenate([p, zp]), np.concatenate([nrm, zn]), np.concatenate([rius, zr]), len(zp)
 
 
-def grazing_rays(spheres, n, rng, ext_frac=0.05, vert_frac=0.08):
+def grazing_rays(spheres, n, rng, ext_frac=0.05, vert_frac=0.08, xaxis_frac=0.0):
     """Rays whose line passes within 1e-9..1e-2 (relative) of a sphere's
     silhouette, on either side, with origins far down the line; a share of
-    near-vertical directions (the prefilter's degenerate basis) and, with
-    ext_frac > 0, direction lengths outside the prefilter's safe range.
-    Returns (n, 6) float32 (origin, direction)."""
+    near-vertical directions, with xaxis_frac > 0 a share of directions near
+    the x axis (the prefilter basis's degenerate direction, rtx_prefilter.h)
+    and, with ext_frac > 0, direction lengths outside the prefilter's safe
+    range. Returns (n, 6) float32 (origin, direction)."""
     sph = np.asarray(spheres, np.float64)
     pick = rng.integers(0, len(sph), n)
     c, r = sph[pick, :3], sph[pick, 3]
@@ -29,6 +30,11 @@ def grazing_rays(spheres, n, rng, ext_frac=0.05, vert_frac=0.08):
     vert = rng.random(n) < vert_frac
     dirs[vert] = np.stack([rng.normal(scale=1e-7, size=vert.sum()), np.sign(rng.normal(size=vert.sum())),
                            rng.normal(scale=1e-7, size=vert.sum())], 1)
+    if xaxis_frac > 0:
+        xa = (rng.random(n) < xaxis_frac) & ~vert
+        eps = 10.0 ** rng.uniform(-9, -3, xa.sum())
+        dirs[xa] = np.stack([np.sign(rng.normal(size=xa.sum())), eps * rng.normal(size=xa.sum()),
+                             eps * rng.normal(size=xa.sum())], 1)
     dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
     e = np.cross(dirs, rng.normal(size=(n, 3)))
     e /= np.linalg.norm(e, axis=1, keepdims=True)

@@ -1,8 +1,8 @@
 // prefilter_check.cpp — CPU check of the exactness claim of the scan's
 // prefilter (raytrace-we-gpu_amd/csrc/rtx_prefilter.h): over many
 // adversarial ray/sphere pairs — near-tangent lines (relative distance
-// 1e-9 .. 1e-1 from the silhouette), tiny and huge directions, near-vertical
-// rays, far origins, centre magnitudes 1e-2 .. 1e4, radii 1e-3 .. 1e3 —
+// 1e-9 .. 1e-1 from the silhouette), tiny and huge directions, rays near
+// the x axis (the basis's degenerate direction) and near the y axis, far origins, centre magnitudes 1e-2 .. 1e4, radii 1e-3 .. 1e3 —
 // whenever the reference's fp32 discriminant is >= 0 or NaN
 // (ShaderCompute.hlsl:158-166; the op order of oracle/rtx_oracle.c
 // hit_world32), the prefilter must flag the sphere — in both op orders the
@@ -51,10 +51,13 @@ int main(int argc, char **argv) {
         const double r = std::pow(10.0, -3.0 + 6.0 * uni());
         unit(dir);
         const double pv = uni();
-        if (pv < 0.05) {  // near-vertical
+        if (pv < 0.04) {  // near the x axis: v = (0, dz, -dy)/|(dy, dz)| degenerates
+            const double eps = std::pow(10.0, -8.0 + 6.0 * uni());
+            dir[1] = eps * sym(), dir[2] = eps * sym(), dir[0] = uni() < 0.5 ? -1.0 : 1.0;
+        } else if (pv < 0.06) {  // near-vertical
             const double eps = std::pow(10.0, -8.0 + 6.0 * uni());
             dir[0] = eps * sym(), dir[2] = eps * sym(), dir[1] = uni() < 0.5 ? -1.0 : 1.0;
-        } else if (pv < 0.08) {  // axis-aligned
+        } else if (pv < 0.09) {  // axis-aligned
             const int ax = (int)(uni() * 3.0) % 3;
             dir[0] = dir[1] = dir[2] = 0.0;
             dir[ax] = uni() < 0.5 ? -1.0 : 1.0;
@@ -96,8 +99,8 @@ int main(int argc, char **argv) {
         const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
         const float R = rtx::prefilter_R(c[0], c[1], c[2], r2);
         const float q = rtx::line_test_q(T, c[0], c[1], c[2], R);
-        // the flat-block order (cy*vy first), as the scan runs it on flat blocks
-        const float qf = rtx::line_test_q_flat(T, rtx::line_test_kv(T, c[1]), c[0], c[2], R);
+        // the flat-block order (the cy terms first), as the scan runs it on flat blocks
+        const float qf = rtx::line_test_q_flat(T, rtx::line_test_flat(T, c[1]), c[0], c[2], R);
         const float disc = ref_disc(o, d, c, -r2, a);
         const bool ref = !(disc < 0.0f);
         const bool flag = !(q < T.thr) && !(qf < T.thr);

@@ -49,7 +49,7 @@ def test_library_built_for_gfx950(rtx):
 
 def test_version_and_error_paths(rtx):
     lib = rtx.load_library()
-    assert lib.rtx_version() == 100
+    assert lib.rtx_version() == 110
     # null arguments are rejected without touching the GPU
     assert lib.rtx_upload_world(None, None) == -1
     assert b"null" in lib.rtx_last_error()
@@ -95,3 +95,27 @@ def test_deinterleave_inverts_partition(rtx, H, T, R):
         ids = rtx.part_row_ids(H, T, p, R)
         g[p, :len(ids)] = img[ids]
     np.testing.assert_array_equal(deinterleave_np(g, H, T, R), img)
+
+
+def test_schedule_defaults_and_validation(rtx):
+    """rtx_schedule (the chain render's schedule): the library's
+    defaults are the measured constants, and rtx_set_schedule validates every
+    field before a context exists (a null ctx is refused first)."""
+    d = rtx.schedule_defaults()
+    assert d.tier1_bar == pytest.approx(1.7) and d.tier1_bar_small == pytest.approx(4.0)
+    assert d.tier1_bar_low == pytest.approx(3.5) and d.tier2_bar_small == pytest.approx(2.0)
+    assert d.tier2_bar_medium == pytest.approx(1.2) and d.small_share == pytest.approx(1.2)
+    assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
+    assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 8
+    assert d.occupancy_small == d.occupancy_low == d.occupancy_normal == 1.0
+    lib = rtx.load_library()
+    assert lib.rtx_set_schedule(None, C.byref(d)) == -1
+    assert lib.rtx_get_schedule(None, C.byref(d)) == -1
+    assert lib.rtx_schedule_defaults(None) == -1
+
+
+def test_library_reads_no_environment(rtx):
+    """The product library takes no tuning from the environment (the
+    schedule is an explicit C-ABI call): no getenv/secure_getenv import."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", rtx.LIB_PATH], capture_output=True, text=True).stdout
+    assert "getenv" not in out, [l for l in out.splitlines() if "getenv" in l]

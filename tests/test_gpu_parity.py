@@ -120,16 +120,68 @@ def test_hit_world_ties_and_padding(gpu_ctx, oracle, rtx):
             assert not np.any(np.isin(want[hit0, 9], [0])), "tie must go to the later duplicate"
 
 
+def test_hit_world_t_range_contract(gpu_ctx, oracle, rtx):
+    """rtx_debug_hit_world's t range: t_min must be finite and > 0 (the
+    resolve orders roots by their bits), t_max < t_min means no hit, a tiny
+    positive t_min is bit-exact against the oracle."""
+    world = rtx.random_world(11, depth=1, spp=1)
+    gpu_ctx.upload_world(world)
+    rng = np.random.default_rng(21)
+    rays = grazing_rays(world.spheres, 3000, rng)
+    for bad in (0.0, -0.0, -1.0, float("nan"), float("inf")):
+        with pytest.raises(rtx.RtxError, match="t_min"):
+            gpu_ctx.debug_hit_world(rays, t_min=bad)
+    with pytest.raises(rtx.RtxError, match="NaN"):
+        gpu_ctx.debug_hit_world(rays, t_max=float("nan"))
+    none = gpu_ctx.debug_hit_world(rays, t_min=2.0, t_max=1.0)
+    assert (none[:, 0] == 0).all() and (none[:, 9] == -1).all()
+    for t_min, t_max in ((1e-30, float("inf")), (1e-3, 7.5), (3.0, 3.0)):
+        got = gpu_ctx.debug_hit_world(rays, t_min=t_min, t_max=t_max)
+        assert_bits_equal(got, oracle.hit_world_f32(world, rays, t_min, t_max), f"t in [{t_min}, {t_max}]")
+
+
+@pytest.mark.parametrize("which", ["c5_100k", "ties"])
+def test_hit_world_wrapped_scan_starts(gpu_ctx, oracle, rtx, which):
+    """The large-scene kernels start a segment's scan where their workgroup's
+    other waves are (pack start) and wrap round ([b0, nblk) then [0, b0)):
+    the resolution rule must give the in-order answer from every start —
+    rtx_debug_hit_world_from at start blocks 0, 1, mid, nblk - 1 and beyond,
+    on the 100k-sphere golden case and on a scene of duplicated spheres
+    whose ties straddle the wrap point."""
+    if which == "c5_100k":
+        c = load_case("hit_c5_100k.npz", 0, lambda ext, cap: rtx.random_world(ext, capacity=cap).spheres)
+        sph, rays, t_min = c["spheres"], c["rays"].astype(np.float32), c["t_min"]
+    else:
+        rng = np.random.default_rng(17)
+        base = np.concatenate([rng.uniform(-8, 8, (700, 1)), rng.uniform(-1, 2, (700, 1)),
+                               rng.uniform(-8, 8, (700, 1)), rng.uniform(0.2, 0.9, (700, 1))], 1)
+        sph = np.concatenate([base, base[::-1]]).astype(np.float32)  # every sphere twice, far apart in index
+        o = rng.uniform(-10, 10, (6000, 3))
+        d = (sph[rng.integers(0, len(sph), 6000), :3] - o) + rng.normal(scale=0.1, size=(6000, 3))
+        rays, t_min = np.concatenate([o, d], 1).astype(np.float32), 0.001
+    n = len(sph)
+    world = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
+    gpu_ctx.upload_world(world)
+    want = oracle.hit_world_f32(world, rays, t_min)
+    nblk = (n + 7) // 8
+    for start in (0, 1, nblk // 2, nblk - 1, nblk + 3):
+        got = gpu_ctx.debug_hit_world(rays, t_min=t_min, start_block=start)
+        assert_bits_equal(got, want, f"{which}: scan from block {start} of {nblk}")
+    if which == "ties":
+        hit = want[:, 9] >= 0
+        assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
+
+
 def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx):
     """Rays whose line passes within 1e-9..1e-2 (relative) of a sphere's
-    silhouette, on either side, plus near-vertical rays (the prefilter's
-    degenerate basis), tiny and huge direction lengths (some outside the
-    prefilter's safe range) and origins far down the line: the kernel's
-    prefiltered scan (rtx_prefilter.h) must return the reference scan's
-    records bit for bit."""
+    silhouette, on either side, plus near-vertical rays and rays near the x
+    axis (the prefilter basis's degenerate direction), tiny and huge
+    direction lengths (some outside the prefilter's safe range) and origins
+    far down the line: the kernel's prefiltered scan (rtx_prefilter.h) must
+    return the reference scan's records bit for bit."""
     rng = np.random.default_rng(11)
     world = rtx.random_world(11, depth=1, spp=1)
-    rays = grazing_rays(world.spheres, 30000, rng)
+    rays = grazing_rays(world.spheres, 30000, rng, xaxis_frac=0.05)
     gpu_ctx.upload_world(world)
     got = gpu_ctx.debug_hit_world(rays)
     want = oracle.hit_world_f32(world, rays)
@@ -276,6 +328,28 @@ def test_c5_scheduled_path_100k_spheres(gpu_ctx, oracle, rtx):
     assert_bits_equal(img, want, "C5 scheduled path")
     assert st.segments == segs
     assert st.samples == 64 * 36 * 16
+
+
+def test_c5_full_width_rows(gpu_ctx, oracle, rtx):
+    """C5 at full size (BASELINE configs[4]: 100k spheres, 1920x1080, spp 16,
+    depth 50) on the bench's schedule: the kPF scan with its pack start,
+    lane mode with 24-entry lists, the 1-spp persistent pre-pass, the tail
+    coop reading the scene from HBM. Two full 1920-px rows bit-exact against
+    the oracle; the frame's segment count (the scheduled render's own
+    counter) equal to the per-pixel counts of an independent exact-grid pass
+    (rtx_debug_pixel_cost), whose sums over those rows equal the oracle's."""
+    W, H = 1920, 1080
+    world = rtx.random_world(159, capacity=100000, depth=50, spp=16)
+    frame = rtx.camera_look_at(W, H)
+    img, st = render_gpu(gpu_ctx, world, frame)
+    assert st.samples == W * H * 16
+    rows = np.array([317, 771], np.uint32)
+    want, segs = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img[rows], want, "C5 rows")
+    assert np.isfinite(img).all()
+    cost = gpu_ctx.debug_pixel_cost(0)
+    assert int(cost.sum(dtype=np.uint64)) == st.segments
+    assert int(cost[rows].sum(dtype=np.uint64)) == segs
 
 
 def test_edge_cases(gpu_ctx, oracle, rtx):
@@ -662,15 +736,16 @@ def test_flat_block_runs_bit_exact(request, oracle, rtx, ctx_name, ext):
 
 @pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
 @pytest.mark.parametrize("coop", [24, 64])
-def test_sphere_major_chunks_bit_exact(request, oracle, rtx, monkeypatch, ctx_name, coop):
+def test_sphere_major_chunks_bit_exact(request, oracle, rtx, ctx_name, coop):
     """Queue exhausted: waves with up to `coop` pixels left trace them with
     the sphere-major group coop in chunks of 8 rays, two rays per packed test
-    (RTX_HEAVY coop=..., read by the host at each launch). An 8-way share of
-    a 320x180 frame (fewer pixels than lanes: every wave starts in the tail)
-    and the whole frame, against the oracle; on the stress build every chunk
-    overflows its pair list and takes the exact sequential path."""
+    (rtx_set_schedule tail_coop_max). An 8-way share of a 320x180 frame
+    (fewer pixels than lanes: every wave starts in the tail) and the whole
+    frame, against the oracle; on the stress build every chunk overflows its
+    pair list and takes the exact sequential path."""
     ctx = request.getfixturevalue(ctx_name)
-    monkeypatch.setenv("RTX_HEAVY", f"coop={coop}")
+    ctx.set_schedule(tail_coop_max=coop)
+    assert ctx.get_schedule().tail_coop_max == coop
     world = rtx.random_world(11, depth=50, spp=10)
     W, H, T = 320, 180, 5
     frame = rtx.camera_look_at(W, H, aspect=W / H)
@@ -685,6 +760,44 @@ def test_sphere_major_chunks_bit_exact(request, oracle, rtx, monkeypatch, ctx_na
         buf.free()
         want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
         assert_bits_equal(got, want, f"{ctx_name} coop={coop} part {part} of {nparts}")
+    ctx.set_schedule()  # back to the defaults
+    assert ctx.get_schedule().tail_coop_max == rtx.schedule_defaults().tail_coop_max
+
+
+def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
+    """rtx_set_schedule refuses out-of-range fields and keeps the previous
+    schedule; extreme but valid schedules (every pixel of a small part in
+    tier 1, no tiers, one wave in ten launched, tail coop of one ray) change
+    only the time: the rows stay bit-exact."""
+    d = rtx.schedule_defaults()
+    for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
+                       ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("reserved", 1)):
+        with pytest.raises(rtx.RtxError):
+            gpu_ctx.set_schedule(**{field: bad})
+        assert gpu_ctx.get_schedule().as_dict() == d.as_dict()
+    world = rtx.random_world(11, depth=50, spp=9)
+    W, H, T = 160, 90, 5
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(frame)
+    extremes = [dict(tier1_bar=0.01, tier1_bar_small=0.01, tier1_bar_low=0.01),
+                dict(tier1_bar=1e6, tier1_bar_small=1e6, tier1_bar_low=1e6, tier2_bar_small=1e6,
+                     tier2_bar_medium=1e6),
+                dict(occupancy_small=0.1, occupancy_low=0.1, occupancy_normal=0.1, hot_fraction=1.0),
+                dict(tail_coop_max=1, hot_fraction=0.0)]
+    for ex in extremes:
+        gpu_ctx.set_schedule()
+        gpu_ctx.set_schedule(**ex)
+        for nparts, part in ((1, 0), (4, 1)):
+            rows = rtx.part_row_ids(H, T, part, nparts)
+            buf = gpu_ctx.alloc((len(rows), W, 4))
+            gpu_ctx.render_rows(T, part, nparts, buf.ptr)
+            got = buf.numpy()
+            buf.free()
+            want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
+            assert_bits_equal(got, want, f"schedule {ex}, part {part} of {nparts}")
+    gpu_ctx.set_schedule()
 
 
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):
@@ -745,12 +858,13 @@ def test_frame_gather_on_torch_default_stream():
 
 def test_cli_writes_reference_frame(tmp_path, oracle, rtx):
     """rtx_cli (the headless DxCSApp driver) renders the frame the oracle renders;
-    its PFM stores rows bottom-to-top like the framebuffer."""
+    its PFM stores rows bottom-to-top like the framebuffer, its PPM the 8-bit
+    image top row first."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cli = os.path.join(root, "raytrace-we-gpu_amd", "bin", "rtx_cli")
-    pfm = str(tmp_path / "f.pfm")
+    pfm, ppm = str(tmp_path / "f.pfm"), str(tmp_path / "f.ppm")
     out = subprocess.run([cli, "--width", "64", "--height", "36", "--spp", "3", "--depth", "50",
-                          "--scene", "rtiow11", "--frames", "1", "--pfm", pfm],
+                          "--scene", "rtiow11", "--frames", "1", "--pfm", pfm, "--ppm", ppm],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     with open(pfm, "rb") as f:
@@ -762,6 +876,12 @@ def test_cli_writes_reference_frame(tmp_path, oracle, rtx):
     frame = rtx.camera_look_at(64, 36, aspect=64 / 36)
     want, _ = oracle.render_rows(world, frame, np.arange(36), nthreads=4)
     assert_bits_equal(img, want[..., :3], "rtx_cli PFM")
+    with open(ppm, "rb") as f:  # 8-bit, top row first, clamped, x 255.999 (Color.h:6-11)
+        assert f.readline().strip() == b"P6" and f.readline().split() == [b"64", b"36"]
+        assert f.readline().strip() == b"255"
+        img8 = np.frombuffer(f.read(), np.uint8).reshape(36, 64, 3)
+    v = np.nan_to_num(want[::-1, :, :3], nan=0.0)
+    np.testing.assert_array_equal(img8, (np.float32(255.999) * np.clip(v, 0, 1).astype(np.float32)).astype(np.uint8))
 
 
 def test_upload_rejects_out_of_range_scene(gpu_ctx, rtx):

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
-"""Sweep the heavy-pixel split's bars (RTX_HEAVY, rtx_kernels.hip
-heavy_tune) on one device: for each setting, the critical part time of an
-R-way row split of C2 (as tools/part_scaling.py). Diagnostic tuning only.
+"""Sweep the chain render's schedule (rtx_set_schedule, include/rtx.h
+rtx_schedule) on one device: for each setting, the critical part time of an
+R-way row split of C2 (as tools/part_scaling.py). A setting is a comma list
+of short names (a1 tier1_bar, a1s tier1_bar_small, a1l tier1_bar_low, a2s
+tier2_bar_small, a2m tier2_bar_medium, rho small_share, rhol low_share, rho2
+medium_share, prio hot_fraction, occs/occl/occn occupancy_small/low/normal,
+coop tail_coop_max) or full field names, applied on top of the defaults.
 
     python tools/heavy_sweep.py --parts 8 --set "a1s=4,a2s=2" --set "a1s=3,a2s=1" ...
 """
@@ -24,6 +28,21 @@ ap.add_argument("--max-spheres", type=int, default=0)
 ap.add_argument("--spp", type=int, default=100)
 a = ap.parse_args()
 
+SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a2s": "tier2_bar_small",
+         "a2m": "tier2_bar_medium", "rho": "small_share", "rhol": "low_share", "rho2": "medium_share",
+         "prio": "hot_fraction", "occs": "occupancy_small", "occl": "occupancy_low", "occn": "occupancy_normal",
+         "coop": "tail_coop_max"}
+
+
+def schedule_of(setting):
+    fields = {}
+    for kv in filter(None, setting.split(",")):
+        k, v = kv.split("=")
+        k = SHORT.get(k.strip(), k.strip())
+        fields[k] = int(v) if k == "tail_coop_max" else float(v)
+    return fields
+
+
 W, H, T = 1920, 1080, 5
 world = rtx.random_world(a.grid, capacity=a.max_spheres or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
@@ -34,10 +53,9 @@ buf = ctx.alloc((H, W, 4))
 sets = a.set or [""]
 for r in range(a.rounds):
     for s in sets:
+        ctx.set_schedule()
         if s:
-            os.environ["RTX_HEAVY"] = s
-        else:
-            os.environ.pop("RTX_HEAVY", None)
+            ctx.set_schedule(**schedule_of(s))
         for R in a.parts:
             times = []
             for p in range(R):
