@@ -163,13 +163,20 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     (< low_share) tier1_bar_low;
  *   - tier 2 (eight pixels per wave): a small part's keys above
  *     tier2_bar_small x share, a MEDIUM part's (< medium_share) above
- *     tier2_bar_medium x share;
+ *     tier2_bar_medium x share, a larger part's above tier2_bar x share
+ *     (tier-2 bars above the tier-1 bar select no tier 2);
  *   - hot_fraction x resident lanes of the normal queue's first slots run at
- *     the top wave priority;
+ *     wave priority hot_priority; tier-1 waves at tier1_priority, tier-2
+ *     waves at tier2_priority (s_setprio 0..3: issue arbitration among the
+ *     waves of a SIMD);
  *   - occupancy_*: the fraction of the resident waves launched for a small /
  *     low / larger part;
  *   - tail_coop_max: once the queue is empty a wave with at most this many
- *     pixels left traces them with several lanes per ray (1..64).
+ *     pixels left traces them with several lanes per ray (1..64);
+ *   - trace_*: for scenes up to 640 spheres tier 1 runs in its own kernel
+ *     beside the render (one pixel per wave, all 64 lanes on its ray), with
+ *     this fraction of the resident waves for a small / low / medium /
+ *     larger part (0: tier 1 stays in the render kernel).
  * Results never depend on the schedule (every pixel's operations are the
  * same whichever lanes trace it); only the time does. The defaults are the
  * measured best. A context starts with the defaults. */
@@ -179,6 +186,7 @@ typedef struct rtx_schedule {
     float tier1_bar_low;      /* default 3.5 */
     float tier2_bar_small;    /* default 2.0 */
     float tier2_bar_medium;   /* default 1.2 */
+    float tier2_bar;          /* default 1e30 (no tier 2 for a larger part) */
     float small_share;        /* default 1.2 pixels per resident lane */
     float low_share;          /* default 2.5 */
     float medium_share;       /* default 3.5 */
@@ -186,14 +194,22 @@ typedef struct rtx_schedule {
     float occupancy_small;    /* default 1.0; each occupancy in (0, 1] */
     float occupancy_low;      /* default 1.0 */
     float occupancy_normal;   /* default 1.0 */
-    uint32_t tail_coop_max;   /* default 8 */
+    float trace_small;        /* default 0; each trace_* in [0, 0.5] */
+    float trace_low;          /* default 0 */
+    float trace_medium;       /* default 0 */
+    float trace_large;        /* default 0 */
+    uint32_t tail_coop_max;   /* default 32 */
+    uint32_t tier1_priority;  /* default 3 */
+    uint32_t tier2_priority;  /* default 2 */
+    uint32_t hot_priority;    /* default 3 */
     uint32_t reserved;        /* must be 0 */
 } rtx_schedule;
 /* The library's defaults (no context, no GPU). */
 RTX_API int rtx_schedule_defaults(rtx_schedule *out);
 /* Validates and installs a schedule for later launches of `ctx` (NULL =
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
- * occupancies in (0, 1], tail_coop_max in 1..64, reserved 0. */
+ * occupancies in (0, 1], trace_* in [0, 0.5], tail_coop_max in 1..64,
+ * priorities in 0..3, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 

@@ -94,6 +94,8 @@ struct rtx_ctx {
     std::vector<EventPair> events = std::vector<EventPair>(kEventRing);  // ring: [ev_head, ev_head + ev_count)
     size_t ev_head = 0, ev_count = 0;
     rtx::KTune tune = rtx::default_tune();  // rtx_set_schedule
+    hipStream_t aux_stream = nullptr;       // k_trace (tier 1 beside the render), created on first use
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     double ms_folded = 0.0;         // durations of launches whose pair was recycled
     uint64_t samples = 0;
     uint64_t launches = 0;
@@ -210,6 +212,9 @@ void rtx_destroy(rtx_ctx *c) {
         if (p.start) (void)hipEventDestroy(p.start);
         if (p.stop) (void)hipEventDestroy(p.stop);
     }
+    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -235,6 +240,7 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->tier1_bar_low = (float)t.a1_low;
     out->tier2_bar_small = (float)t.a2_small;
     out->tier2_bar_medium = (float)t.a2_medium;
+    out->tier2_bar = (float)std::min(t.a2_large, 1e30);
     out->small_share = (float)t.rho;
     out->low_share = (float)t.rho_low;
     out->medium_share = (float)t.rho2;
@@ -243,6 +249,13 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->occupancy_low = (float)t.occ_low;
     out->occupancy_normal = (float)t.occ_normal;
     out->tail_coop_max = t.coop_max;
+    out->trace_small = (float)t.trace_small;
+    out->trace_low = (float)t.trace_low;
+    out->trace_medium = (float)t.trace_medium;
+    out->trace_large = (float)t.trace_large;
+    out->tier1_priority = t.prio_t1;
+    out->tier2_priority = t.prio_t2;
+    out->hot_priority = t.prio_hot;
     return RTX_OK;
 }
 
@@ -255,7 +268,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     const struct { const char *name; float v; } pos[] = {
         {"tier1_bar", s->tier1_bar},         {"tier1_bar_small", s->tier1_bar_small},
         {"tier1_bar_low", s->tier1_bar_low}, {"tier2_bar_small", s->tier2_bar_small},
-        {"tier2_bar_medium", s->tier2_bar_medium}, {"small_share", s->small_share},
+        {"tier2_bar_medium", s->tier2_bar_medium}, {"tier2_bar", s->tier2_bar}, {"small_share", s->small_share},
         {"low_share", s->low_share},         {"medium_share", s->medium_share}};
     for (const auto &f : pos)
         if (!(f.v > 0.0f && f.v <= 1e30f))
@@ -267,6 +280,11 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         if (!(o > 0.0f && o <= 1.0f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: occupancies must be in (0, 1]");
     if (s->tail_coop_max < 1 || s->tail_coop_max > 64)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max must be in 1..64");
+    const float tr[] = {s->trace_small, s->trace_low, s->trace_medium, s->trace_large};
+    for (float v : tr)
+        if (!(v >= 0.0f && v <= 0.5f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_* must be in [0, 0.5]");
+    if (s->tier1_priority > 3 || s->tier2_priority > 3 || s->hot_priority > 3)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: priorities must be in 0..3");
     if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
     rtx::KTune t;
     t.a1 = s->tier1_bar;
@@ -274,6 +292,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.a1_low = s->tier1_bar_low;
     t.a2_small = s->tier2_bar_small;
     t.a2_medium = s->tier2_bar_medium;
+    t.a2_large = s->tier2_bar;
     t.rho = s->small_share;
     t.rho_low = s->low_share;
     t.rho2 = s->medium_share;
@@ -282,6 +301,13 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.occ_low = s->occupancy_low;
     t.occ_normal = s->occupancy_normal;
     t.coop_max = s->tail_coop_max;
+    t.trace_small = s->trace_small;
+    t.trace_low = s->trace_low;
+    t.trace_medium = s->trace_medium;
+    t.trace_large = s->trace_large;
+    t.prio_t1 = s->tier1_priority;
+    t.prio_t2 = s->tier2_priority;
+    t.prio_hot = s->hot_priority;
     c->tune = t;
     return RTX_OK;
 }
@@ -295,6 +321,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->tier1_bar_low = (float)t.a1_low;
     out->tier2_bar_small = (float)t.a2_small;
     out->tier2_bar_medium = (float)t.a2_medium;
+    out->tier2_bar = (float)std::min(t.a2_large, 1e30);
     out->small_share = (float)t.rho;
     out->low_share = (float)t.rho_low;
     out->medium_share = (float)t.rho2;
@@ -303,6 +330,13 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->occupancy_low = (float)t.occ_low;
     out->occupancy_normal = (float)t.occ_normal;
     out->tail_coop_max = t.coop_max;
+    out->trace_small = (float)t.trace_small;
+    out->trace_low = (float)t.trace_low;
+    out->trace_medium = (float)t.trace_medium;
+    out->trace_large = (float)t.trace_large;
+    out->tier1_priority = t.prio_t1;
+    out->tier2_priority = t.prio_t2;
+    out->hot_priority = t.prio_hot;
     return RTX_OK;
 }
 
@@ -600,6 +634,14 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     sched.npix = (uint32_t)c->sched_pixels;
     sched.nbuckets = rtx::kCostBuckets;
     sched.tune = c->tune;
+    if (!c->aux_stream) {
+        RTX_HIP(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        RTX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        RTX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    sched.aux = c->aux_stream;
+    sched.ev_fork = c->ev_fork;
+    sched.ev_join = c->ev_join;
     hipError_t e = rtx::launch_render(p, sched, c->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_render");
     RTX_HIP(hipEventRecord(ev.stop, c->stream));

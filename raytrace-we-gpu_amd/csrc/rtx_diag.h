@@ -105,8 +105,7 @@ struct Diag {
         const unsigned long long tn = __builtin_readcyclecounter();
         if (was_coop) cpa[4] += tn - ctq;
         ctq = tn;
-        cpa[5]++;
-        return cpa;
+        return cpa;  // the coop code counts its segments in cpa[5]
 #else
         (void)tier;
         tqp = nullptr;

@@ -66,6 +66,8 @@ struct KParams {
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
     uint32_t coop_max;             // queue exhausted: a wave with <= this many pixels traces them in group coop
+    uint32_t prio_t1, prio_t2, prio_hot;  // wave priorities (0..3) of tier-1, tier-2 and hot lane-mode waves
+    uint32_t trace_ext;            // tier 1 runs in k_trace beside k_render (k_render skips it)
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
@@ -83,9 +85,11 @@ struct KParams {
 // fraction, launch occupancy, tail-coop size. Doubles: k_heavy_split
 // compares them with sums of cost keys.
 struct KTune {
-    double a1, a1_small, a1_low, a2_small, a2_medium, rho, rho_low, rho2, prio_frac;
+    double a1, a1_small, a1_low, a2_small, a2_medium, a2_large, rho, rho_low, rho2, prio_frac;
     double occ_small, occ_low, occ_normal;  // fraction of the resident waves launched for a small / low / larger share
     uint32_t coop_max;                      // KParams::coop_max
+    uint32_t prio_t1, prio_t2, prio_hot;    // KParams::prio_*
+    double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
 };
 KTune default_tune();
 
@@ -99,6 +103,8 @@ struct KSchedule {
     float *ps_scratch;  // k_render_ps scratch (rng_mode 1), ps_floats floats
     size_t ps_floats;
     KTune tune;
+    hipStream_t aux;    // k_trace's stream (NULL: tier 1 stays in k_render)
+    hipEvent_t ev_fork, ev_join;
 };
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)

@@ -78,7 +78,8 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 // Makefile variants prof/ptime/cprof); the candidate-list capacities below
 // are also set by the stress build. Everything else is a fixed product
 // constant.
-constexpr int kCoopMax = 8;             // tail mode: a wave with <= this many active lanes traces their rays together
+constexpr int kCoopMax = 32;            // tail mode: a wave with <= this many active lanes traces their rays together
+                                        // (8 -> 32 with the sphere-pair coop: parts 1/4/8 -0.8..1.5 ms, R3e)
 constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wave
 constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
 constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha * a lane's share of the summed keys
@@ -89,6 +90,12 @@ constexpr double kHeavy1AlphaLow = 3.5;     // tier-1 bar for a low share (DESIG
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > this * share (2-way split: 37 -> 34 ms, r5a-b)
+constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (default: none)
+// k_trace waves (tier 1 outside k_render) as a fraction of the resident waves, by share class.
+// Measured (profiles/R3h_*): parts 8 / 4 / 2 are no faster with it (15.0-15.2 ms in-kernel vs
+// 16.2-16.6 with 20 %; 20.3 both; 30.7 vs 44 with 5 %: its few waves queue the many medium-share
+// tier-1 pixels), so it is off there; the whole frame is R3i.
+constexpr double kTraceSmall = 0.0, kTraceLow = 0.0, kTraceMedium = 0.0, kTraceLarge = 0.0;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -586,7 +593,7 @@ struct SphGlobal {
 // Build the block's LDS copy (all threads of the block; the caller
 // synchronises): sphere i < npad at pair i/2, slot i%2 (copies of n - 1
 // beyond n), radii after the pairs.
-__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on) {
+__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on, uint32_t nthreads = kRB) {
     SphLds l;
     l.n = S.n;
     l.npairs = coop_npad(S.n) / 2u;
@@ -594,7 +601,7 @@ __device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on
     l.rad = base + 8u * l.npairs;
     if (on) {
         float *pr = base, *rad = base + 8u * l.npairs;
-        for (uint32_t i = threadIdx.x; i < 2u * l.npairs; i += kRB) {
+        for (uint32_t i = threadIdx.x; i < 2u * l.npairs; i += nthreads) {
             const float4 c = S.pre4[min(i, S.n - 1u)];
             float *q = pr + 8u * (i >> 1) + (i & 1u);
             q[0] = c.x;
@@ -618,8 +625,12 @@ __device__ __forceinline__ SphGlobal sph_global(const KScene &S) {
 // Reduction over aligned groups of 2^lg lanes (lg wave-uniform, whole wave
 // active): DPP inside a row of 16 (quad_perm xor 1 and xor 2, then the
 // half-row and row mirrors, which pair each lane with one in the other half),
-// ds_swizzle xor 16, ds_bpermute xor 32. Every lane of a group ends with the
-// group's min (or max).
+// then gfx950's v_permlane16_swap (rows 2i <-> 2i + 1: xor 16) and
+// v_permlane32_swap (halves: xor 32) — VALU exchanges, no LDS round trip.
+// With both operands the same register, a swap leaves each lane with its
+// own value in one result and its partner's in the other, so op(r0, r1) is
+// the xor-16 / xor-32 step. Every lane of a group ends with the group's min
+// (or max).
 template <bool kMax>
 __device__ __forceinline__ uint32_t group_reduce_u32(uint32_t v, uint32_t lg) {
     auto op = [](uint32_t x, uint32_t y) { return kMax ? max(x, y) : min(x, y); };
@@ -627,8 +638,14 @@ __device__ __forceinline__ uint32_t group_reduce_u32(uint32_t v, uint32_t lg) {
     if (lg >= 2u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
     if (lg >= 3u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
     if (lg >= 4u) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
-    if (lg >= 5u) v = op(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F));
-    if (lg >= 6u) v = op(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+    if (lg >= 5u) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = op((uint32_t)r[0], (uint32_t)r[1]);
+    }
+    if (lg >= 6u) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = op((uint32_t)r[0], (uint32_t)r[1]);
+    }
     return v;
 }
 
@@ -683,6 +700,7 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
             w[7] = inv_a;
         }
         __builtin_amdgcn_wave_barrier();
+        if (RTX_DIAG_COOP && cp && c0 == 0u) cp[5]++;
         RTX_CP(0)
         const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
         const uint32_t g = 1u << lg;
@@ -862,22 +880,62 @@ enum { kSegContinue = 0, kSegSky = 1, kSegBlack = 2 };
 //    and baseHash of it; the lane then converts the hash as its call would;
 //  * sqrt(1 - x*x): random_in_unit_sphere's sqrt(1 - h.x^2) (:63) and the
 //    dielectric's sin_theta = sqrt(1 - cos_theta^2) (:234).
-template <typename LaneT>
-__device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit, float t, f3 &sky_col) {
-    const KScene &S = P.scene;
+// The seed-determined part of a Lambert/metal scatter (random_in_unit_sphere,
+// :59-66): the hash step and everything computed from it before the hit is
+// known — the wave-wide pixel trace (trace_pixel_wave) evaluates it before
+// the scan, off the segment's critical path. The same ops as path_segment's
+// own evaluation, so the same bits; discarded when the segment does not
+// scatter (the seed then does not advance).
+struct ScatterSpec {
+    float seed;   // after the hash step
+    uint32_t hn;  // the step's baseHash
+    float hx, sq, r, sn, cs;
+};
+__device__ __forceinline__ ScatterSpec scatter_spec(float seed) {
+    ScatterSpec s;
+    s.seed = seed;
+    s.hn = hash_step(s.seed);
+    s.hx = ((float)(s.hn & 0x7fffffffu) / 2147483648.0f) * 2.0f - 1.0f;
+    const float phi = ((float)((s.hn * 16807u) & 0x7fffffffu) / 2147483648.0f) * 6.28318530718f;
+    const float hz = (float)((s.hn * 48271u) & 0x7fffffffu) / 2147483648.0f;
+    s.sq = sqrt_rn(1.0f - s.hx * s.hx);
+    s.r = pow_rt(hz, 0.333333333f);
+    sincos_rt(phi, s.sn, s.cs);
+    return s;
+}
+
+// The hit sphere's record inputs: (centre, radius), material code, values.
+struct HitMat {
+    float4 sc;
+    int mt;
+    float4 mv;
+};
+__device__ __forceinline__ HitMat hit_mat(const KScene &S, int hit) {
+    HitMat m;
+    m.sc = S.cen[hit];
+    m.mt = S.mtype[hit];
+    m.mv = S.mval[hit];
+    return m;
+}
+
+// path_segment with the hit's record inputs given (hit >= 0; M unused on a
+// miss) and, with kSpec, the scatter's seed-determined part precomputed.
+template <bool kSpec, typename LaneT>
+__device__ __forceinline__ int path_segment_m(const KParams &P, LaneT &L, int hit, float t, const HitMat &M,
+                                              const ScatterSpec &sp, f3 &sky_col) {
     int mt = 3;
     f3 p = L.o, nrm = L.d;
     bool ff = false;
     float4 mv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (hit >= 0) {
-        const float4 sc = S.cen[hit];
+        const float4 sc = M.sc;
         p = L.o + t * L.d;                             // Ray::at, Ray.h:16-19
         const float inv_r = 1.0f / sc.w;               // Vec3 operator/, Vec3.h:83-86
         nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));     // Sphere.cpp:28
         ff = dot3(L.d, nrm) < 0.0f;                    // set_face_normal, :143-150
         if (!ff) nrm = -nrm;
-        mt = S.mtype[hit];
-        mv = S.mval[hit];
+        mt = M.mt;
+        mv = M.mv;
     }
     const bool sky = hit < 0;
     const bool diel = !sky && mt == 2;
@@ -891,19 +949,27 @@ __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit,
         return kSegSky;
     }
     if (mt != 0 && mt != 1 && !diel) return kSegBlack;  // unknown material: sample is black (:251, :274)
-    const uint32_t hn = hash_step(L.seed);
+    uint32_t hn;
+    if constexpr (kSpec) {
+        hn = sp.hn;
+        L.seed = sp.seed;
+    } else {
+        hn = hash_step(L.seed);
+    }
     float x, cosine = 0.0f, ratio = 0.0f, hx = 0.0f, phi = 0.0f, hz = 0.0f;
     if (diel) {  // DIELECTRIC (:229-249), atten = 1
         ratio = ff ? (1.0f / mv.w) : mv.w;
         cosine = fminf(dot3(-ud, nrm), 1.0f);
         x = cosine;
-    } else {     // random_in_unit_sphere's hash3 (:43-48, :59-66)
+    } else if constexpr (!kSpec) {  // random_in_unit_sphere's hash3 (:43-48, :59-66)
         hx = ((float)(hn & 0x7fffffffu) / 2147483648.0f) * 2.0f - 1.0f;
         phi = ((float)((hn * 16807u) & 0x7fffffffu) / 2147483648.0f) * 6.28318530718f;
         hz = (float)((hn * 48271u) & 0x7fffffffu) / 2147483648.0f;
         x = hx;
+    } else {
+        x = sp.hx;
     }
-    const float sq = sqrt_rn(1.0f - x * x);
+    const float sq = (kSpec && !diel) ? sp.sq : sqrt_rn(1.0f - x * x);
     f3 dir;
     if (diel) {
         const bool cant = ratio * sq > 1.0f;
@@ -914,9 +980,16 @@ __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit,
     } else {
         // Lambert and metal share random_in_unit_sphere and normalize: run
         // them once for both kinds of lane (each lane's ops are the HLSL's).
-        const float r = pow_rt(hz, 0.333333333f);
-        float sn, cs;
-        sincos_rt(phi, sn, cs);
+        float r, sn, cs;
+        if constexpr (kSpec) {
+            r = sp.r;
+            sn = sp.sn;
+            cs = sp.cs;
+            hx = sp.hx;
+        } else {
+            r = pow_rt(hz, 0.333333333f);
+            sincos_rt(phi, sn, cs);
+        }
         const f3 rius = f3{r * (sq * sn), r * (sq * cs), r * hx};
         const f3 v = mt == 0 ? ((p + nrm) + rius) - p                // DIFFUSE (:209-217)
                              : reflect3(L.d, nrm) + mv.w * rius;     // METAL (:219-227)
@@ -929,6 +1002,12 @@ __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit,
     L.inv_a = 1.0f / L.a;
     L.bounce++;
     return L.bounce >= P.depth ? kSegBlack : kSegContinue;  // depth exhausted -> black (:286)
+}
+template <typename LaneT>
+__device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit, float t, f3 &sky_col) {
+    HitMat M;
+    if (hit >= 0) M = hit_mat(P.scene, hit);
+    return path_segment_m<false>(P, L, hit, t, M, ScatterSpec{}, sky_col);
 }
 
 // Chain-RNG lane: one segment, then the pixel's next sample when the path
@@ -1002,6 +1081,16 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
     begin_sample(P, F, L.x, L.y, L);
 }
 
+// s_setprio takes an immediate: a wave-uniform priority 0..3 by branch.
+__device__ __forceinline__ void set_prio(uint32_t p) {
+    switch (__builtin_amdgcn_readfirstlane(p)) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 // Persistent-lane pixel queue: every idle lane of the wave takes the next
 // slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
 // per refill (ballot + lane rank). Returns true once the queue is
@@ -1073,6 +1162,114 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
         H.tier = 2;
 }
 
+// ---- one pixel traced by the whole wave: tier 1 (k_trace) -----------------
+// A pixel whose chain is the critical path of the frame (or of a rank's
+// share) is traced to its end by all 64 lanes of a wave: every lane holds
+// the same Lane state, lane k scans sphere pairs k, k + 64, ... (the group
+// coop's scan with g = 64, from the LDS copy), the wave reduces (min c, then
+// the largest index among equal c: the in-order scan's answer) and shades
+// uniformly with the lane-mode functions. Taken off each segment's critical
+// path: the scatter's seed-determined part (scatter_spec) is evaluated before
+// the scan, and each lane loads the material of its own best candidate while
+// the wave reduces; the winner's is then read from its lane. A non-finite
+// root takes the exact in-order scan (every lane the same ray). W: the
+// pixel's state after start_pixel, the same in every lane; on return the
+// pixel's samples are done (W.acc, W.seed, W.segs final).
+template <typename Src>
+__device__ __forceinline__ void trace_pixel_uniform(const KParams &P, const Frame &F, const Src &src, Lane &W,
+                                                    unsigned long long *cp, unsigned long long *tq) {
+    const KScene &S = P.scene;
+    const uint32_t lane = threadIdx.x & 63u;
+    const float inf = __uint_as_float(0x7f800000u);
+    const int last = (int)S.n - 1;
+    const uint32_t plast = src.npairs - 1u;
+    const uint32_t nsteps = (src.npairs + 63u) >> 6;
+    for (;;) {
+        RTX_CP(4)
+        if (RTX_DIAG_COOP && cp) cp[5]++;
+        const ScatterSpec sp = scatter_spec(W.seed);
+        const LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
+        const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+        const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
+        uint64_t key = hit_key(inf, -1);
+        bool ok = true;
+        RTX_CP(0)
+#pragma unroll 1
+        for (uint32_t s0 = 0; s0 < nsteps; s0 += kGfSteps) {
+            // the group coop's scan and resolve (hit_world_groups) with g = 64
+            uint32_t im = 0;
+            const uint32_t s1 = min(s0 + kGfSteps, nsteps);
+            auto step = [&](uint32_t st) {
+                f2v cx, cy, cz, R;
+                src.pair(Src::kPadded ? (st << 6) + lane : min((st << 6) + lane, plast), cx, cy, cz, R);
+                const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+                const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
+                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
+                im = (im << 1) | (__float_as_uint(q.y) >> 31);
+                im = (im << 1) | (__float_as_uint(q.x) >> 31);
+            };
+            uint32_t st = s0;
+            for (; st + 2u <= s1; st += 2u) {
+                step(st);
+                step(st + 1u);
+            }
+            if (st < s1) step(st);
+            const uint32_t nb = 2u * (s1 - s0);
+            uint32_t fm = ~im & (nb >= 32u ? ~0u : ((1u << nb) - 1u));
+#pragma unroll 1
+            while (__ballot(fm != 0u) != 0ull) {
+                const bool live = fm != 0u;
+                const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
+                fm &= fm - 1u;
+                const uint32_t p = ((s1 - 1u - (bit >> 1)) << 6) + lane;
+                const uint32_t j = 2u * (Src::kPadded ? p : min(p, plast)) + (bit & 1u);
+                resolve_one(src.sphere(j), (int)j, live, W.o, W.d, W.a, W.inv_a, kTMin, key, ok);
+            }
+        }
+        RTX_CP(1)
+        // each lane's best candidate: its material is loaded during the reduction
+        const uint32_t lo = ~(uint32_t)key;  // index + 1, 0: none
+        const uint32_t jl = lo != 0u ? min(lo - 1u, (uint32_t)last) : 0u;
+        const int mt_l = S.mtype[jl];
+        const float4 mv_l = S.mval[jl];
+        const uint32_t cb0 = (uint32_t)(key >> 32);
+        const uint32_t cb = group_reduce_u32<false>(cb0, 6u);
+        const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? lo : 0u, 6u);
+        int hit = -1;
+        float t = inf;
+        HitMat M;
+        if (__ballot(!ok) != 0ull) {  // a non-finite root: the exact in-order scan
+            hit = hit_blocks_seq((cfloat_p)S.soa, S.n_pad / 8u, 0, W.o, W.d, W.a, W.inv_a, kTMin, t, -1);
+            if (hit >= 0) {
+                hit = min(hit, last);
+                M = hit_mat(S, hit);
+            }
+        } else if (ib != 0u) {
+            hit = min((int)(ib - 1u), last);
+            t = __uint_as_float(cb);
+            const int wl = __builtin_ctzll(__ballot(lo == ib && cb0 == cb));  // a lane holding the winner
+            M.sc = src.sphere((uint32_t)hit);  // the same floats as cen[hit]
+            M.mt = __builtin_amdgcn_readlane(mt_l, wl);
+            M.mv = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.x), wl)),
+                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.y), wl)),
+                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.z), wl)),
+                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.w), wl)));
+        }
+        RTX_CP(2)
+        W.segs++;
+        f3 c;
+        const int r = path_segment_m<true>(P, W, hit, t, M, sp, c);
+        if (r == kSegSky) W.acc = W.acc + c;
+        if (r != kSegContinue) {
+            W.sample++;
+            if (W.sample >= P.spp) break;
+            begin_sample(P, F, W.x, W.y, W);
+        }
+        RTX_CP(3)
+    }
+    RTX_CP(3)
+}
+
 // Render kernel (chain RNG), per-wave independent; sphere blocks are read
 // with scalar loads (a block-wide LDS copy serves the coop and the resolve of
 // scenes up to kCoopLds spheres). kPersist: the grid holds as many waves as the GPU keeps resident and
@@ -1116,7 +1313,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     HeavyState H;
     H.kh = (kPersist && P.heavy) ? min(P.heavy[1], npix) : 0u;
     H.k1 = (kPersist && P.heavy) ? min(P.heavy[3], H.kh) : 0u;
-    H.t1_done = H.k1 == 0u;
+    H.t1_done = H.k1 == 0u || P.trace_ext != 0u;  // tier 1: k_trace when it runs beside this kernel
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
@@ -1138,12 +1335,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             float my_best = __uint_as_float(0x7f800000u);
             bool my_seq = false;
             // this wave carries the frame's critical path: tier 1 > tier 2 > tail
-            if (H.tier == 1u)
-                __builtin_amdgcn_s_setprio(3);
-            else if (H.tier == 2u)
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(kTailPrio);
+            set_prio(H.tier == 1u ? P.prio_t1 : H.tier == 2u ? P.prio_t2 : (uint32_t)kTailPrio);
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
             int my_hit = coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
@@ -1165,10 +1357,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
-        if (__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull)
-            __builtin_amdgcn_s_setprio(3);
-        else
-            __builtin_amdgcn_s_setprio(0);
+        set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
@@ -1190,6 +1379,43 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         P.wave_times[2 * w] = t_start;
         P.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// Tier 1 as its own kernel (the scheduled path, scenes up to kCoopLds
+// spheres): single-wave workgroups launched on the context's auxiliary
+// stream beside k_render (launch_render), each taking tier-1 slots ([0, k1)
+// of the cost-ordered queue, k_heavy_split) one at a time and tracing the
+// pixel with the whole wave (trace_pixel_uniform), at wave priority
+// prio_t1. Its own register budget (up to 128 VGPRs) keeps the wave trace's
+// state out of k_render, whose lane-mode loop it would otherwise crowd into
+// scratch. k_render skips tier 1 (KParams::trace_ext).
+constexpr uint32_t kTraceThreads = 64;
+__global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem), true, kTraceThreads);
+    __syncthreads();
+    const Frame F = load_frame(P);
+    const uint32_t npix = P.rows_local * P.width;
+    const uint32_t k1 = min(P.heavy[3], min(P.heavy[1], npix));
+    set_prio(P.prio_t1);
+    uint32_t segs = 0;
+    for (;;) {
+        uint32_t slot = 0;
+        if (threadIdx.x == 0) slot = atomicAdd(P.heavy, 1u);  // the tier-1 counter
+        slot = (uint32_t)__shfl((int)slot, 0, 64);
+        if (slot >= k1) break;
+        Lane W;
+        W.segs = 0;
+        start_pixel(P, F, P.perm[slot], W);
+        diag_pixel_start(P, W.gid, 1ull);
+        trace_pixel_uniform(P, F, sl, W, nullptr, nullptr);
+        if (threadIdx.x == 0) {
+            write_pixel<false>(P, W);
+            diag_pixel_end(P, W.gid);
+        }
+        segs += W.segs;
+    }
+    if (threadIdx.x == 0 && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
 }
 
 // ---- cost-ordered pixel queue (LPT scheduling, see KSchedule) ------------
@@ -1288,12 +1514,20 @@ KTune default_tune() {
     t.a1_low = kHeavy1AlphaLow;
     t.a2_small = kHeavyAlpha;
     t.a2_medium = kHeavy2AlphaMedium;
+    t.a2_large = kHeavy2AlphaLarge;
     t.rho = kHeavyRho;
     t.rho_low = kHeavyRhoLow;
     t.rho2 = kHeavyRho2;
     t.prio_frac = kPrioFracX100 / 100.0;
     t.occ_small = t.occ_low = t.occ_normal = 1.0;
     t.coop_max = (uint32_t)kCoopMax;
+    t.prio_t1 = 3;
+    t.prio_t2 = 2;
+    t.prio_hot = 3;
+    t.trace_small = kTraceSmall;
+    t.trace_low = kTraceLow;
+    t.trace_medium = kTraceMedium;
+    t.trace_large = kTraceLarge;
     return t;
 }
 namespace {
@@ -1312,7 +1546,7 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     // a medium share (fewer than rho2 pixels per lane, e.g. a
     // 2- or 4-way split) also gets tier 2 above a2_medium x share
     const bool medium = !small && (double)npix < t.rho2 * (double)lanes;
-    const double a2 = small ? t.a2_small : medium ? min(t.a2_medium, a1) : a1;
+    const double a2 = small ? t.a2_small : medium ? min(t.a2_medium, a1) : min(t.a2_large, a1);
     uint32_t kh = 0, k1 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
@@ -1753,6 +1987,9 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     const KTune &tune = sched.tune;  // validated by rtx_set_schedule
     KParams p = p_in;
     p.coop_max = min(max(tune.coop_max, 1u), 64u);
+    p.prio_t1 = tune.prio_t1;
+    p.prio_t2 = tune.prio_t2;
+    p.prio_hot = tune.prio_hot;
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t need = ceil_div(lanes, kRB);
@@ -1823,8 +2060,32 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.heavy = heavy;
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    // tier 1 in k_trace on the auxiliary stream (small scenes): its waves
+    // are launched first and k_render leaves room for them (trace_waves / 4
+    // fewer blocks), so whichever dispatches first, both are resident.
+    uint32_t trace_waves = 0;
+    if (sched.aux && !pf && p.scene.n <= kCoopLds) {
+        const double px_per_lane = (double)lanes / ((double)blocks * kRB);
+        const double frac = px_per_lane < tune.rho ? tune.trace_small : px_per_lane < tune.rho_low ? tune.trace_low
+                            : px_per_lane < tune.rho2 ? tune.trace_medium : tune.trace_large;
+        trace_waves = (uint32_t)(frac * blocks * (kRB / 64) + 0.5);
+    }
+    if (trace_waves > 0) {
+        q.trace_ext = 1u;
+        const size_t tlds = coop_lds_bytes(p.scene.n);
+        e = hipEventRecord(sched.ev_fork, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sched.aux, sched.ev_fork, 0);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_trace, dim3(trace_waves), dim3(kTraceThreads), tlds, sched.aux, q);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(sched.ev_join, sched.aux);
+        if (e != hipSuccess) return e;
+        blocks = max(1u, blocks - (trace_waves + 3u) / 4u);
+    }
     launch_k<true, false>(pf, blocks, lds, stream, q);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess && trace_waves > 0) e = hipStreamWaitEvent(stream, sched.ev_join, 0);
+    return e;
 }
 
 hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t width,

@@ -55,10 +55,14 @@ class rtx_frame(C.Structure):
 class rtx_schedule(C.Structure):
     """The chain render's schedule (include/rtx.h rtx_schedule)."""
     _fields_ = [("tier1_bar", C.c_float), ("tier1_bar_small", C.c_float), ("tier1_bar_low", C.c_float),
-                ("tier2_bar_small", C.c_float), ("tier2_bar_medium", C.c_float), ("small_share", C.c_float),
+                ("tier2_bar_small", C.c_float), ("tier2_bar_medium", C.c_float), ("tier2_bar", C.c_float),
+                ("small_share", C.c_float),
                 ("low_share", C.c_float), ("medium_share", C.c_float), ("hot_fraction", C.c_float),
                 ("occupancy_small", C.c_float), ("occupancy_low", C.c_float), ("occupancy_normal", C.c_float),
-                ("tail_coop_max", C.c_uint32), ("reserved", C.c_uint32)]
+                ("trace_small", C.c_float), ("trace_low", C.c_float), ("trace_medium", C.c_float),
+                ("trace_large", C.c_float),
+                ("tail_coop_max", C.c_uint32), ("tier1_priority", C.c_uint32), ("tier2_priority", C.c_uint32),
+                ("hot_priority", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}

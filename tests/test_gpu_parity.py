@@ -772,7 +772,8 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("reserved", 1)):
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1),
+                       ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})
         assert gpu_ctx.get_schedule().as_dict() == d.as_dict()
@@ -785,7 +786,12 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
                 dict(tier1_bar=1e6, tier1_bar_small=1e6, tier1_bar_low=1e6, tier2_bar_small=1e6,
                      tier2_bar_medium=1e6),
                 dict(occupancy_small=0.1, occupancy_low=0.1, occupancy_normal=0.1, hot_fraction=1.0),
-                dict(tail_coop_max=1, hot_fraction=0.0)]
+                dict(tail_coop_max=1, hot_fraction=0.0),
+                dict(tier1_priority=0, tier2_priority=1, hot_priority=2, tier2_bar=0.5),
+                dict(trace_small=0.0, trace_low=0.0, trace_medium=0.0, trace_large=0.0, tier1_bar=0.01,
+                     tier1_bar_small=0.01, tier1_bar_low=0.01),
+                dict(trace_small=0.5, trace_low=0.5, trace_medium=0.5, trace_large=0.5, tier1_bar=0.01,
+                     tier1_bar_small=0.01, tier1_bar_low=0.01)]
     for ex in extremes:
         gpu_ctx.set_schedule()
         gpu_ctx.set_schedule(**ex)

@@ -28,19 +28,7 @@ ap.add_argument("--max-spheres", type=int, default=0)
 ap.add_argument("--spp", type=int, default=100)
 a = ap.parse_args()
 
-SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a2s": "tier2_bar_small",
-         "a2m": "tier2_bar_medium", "rho": "small_share", "rhol": "low_share", "rho2": "medium_share",
-         "prio": "hot_fraction", "occs": "occupancy_small", "occl": "occupancy_low", "occn": "occupancy_normal",
-         "coop": "tail_coop_max"}
-
-
-def schedule_of(setting):
-    fields = {}
-    for kv in filter(None, setting.split(",")):
-        k, v = kv.split("=")
-        k = SHORT.get(k.strip(), k.strip())
-        fields[k] = int(v) if k == "tail_coop_max" else float(v)
-    return fields
+from heavy_sweep_fields import schedule_of  # noqa: E402
 
 
 W, H, T = 1920, 1080, 5

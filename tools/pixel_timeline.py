@@ -23,12 +23,16 @@ ap.add_argument("lib")
 ap.add_argument("--parts", type=int, nargs="*", default=[1, 2, 8])
 ap.add_argument("--which", type=int, default=0, help="part index to trace (mod R)")
 ap.add_argument("--tile-rows", type=int, default=5)
+ap.add_argument("--set", default="", help="schedule fields (tools/heavy_sweep.py syntax), e.g. a1=1.5,coop=32")
 a = ap.parse_args()
 
 W, H, T = 1920, 1080, a.tile_rows
 world = rtx.random_world(11, depth=50, spp=100)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
 ctx = rtx.Context(0, lib=rtx.load_library(a.lib))
+if a.set:
+    from heavy_sweep_fields import schedule_of
+    ctx.set_schedule(**schedule_of(a.set))
 ctx.upload_world(world)
 ctx.set_frame(frame)
 cost = ctx.debug_pixel_cost().astype(np.int64)  # (H, W) segments per pixel
@@ -70,7 +74,7 @@ for R in a.parts:
                              "start_us_max": round(float(s_us[sel].max()), 1),
                              "end_us_max": round(float(e_us[sel].max()), 1)}
     late = ok & (e_us > 0.9 * span)
-    out = {"parts": R, "part": p, "pixels": npix, "kernel_ms": round(st.kernel_ms / max(1, st.launches), 3),
+    out = {"set": a.set or "default", "parts": R, "part": p, "pixels": npix, "kernel_ms": round(st.kernel_ms / max(1, st.launches), 3),
            "span_us": round(span, 1), "segments_total": int(seg.sum()), "segments_max": int(seg.max()),
            "modes": modes, "last_finishing": [rec(i) for i in last], "heaviest": [rec(i) for i in heavy],
            "late10pct": {"pixels": int(late.sum()), "segments_mean": round(float(seg[late].mean()), 1) if late.any() else 0,
