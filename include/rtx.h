@@ -176,7 +176,12 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *   - trace_*: for scenes up to 640 spheres tier 1 runs in its own kernel
  *     beside the render (one pixel per wave, all 64 lanes on its ray), with
  *     this fraction of the resident waves for a small / low / medium /
- *     larger part (0: tier 1 stays in the render kernel).
+ *     larger part (0: tier 1 stays in the render kernel);
+ *   - promote_*: once the pixel queue is empty, a lane whose pixel is
+ *     projected to need more than this many further ray segments hands it
+ *     over at a sample boundary to a wave with nothing else to do (an idle
+ *     render wave, or the tier-1 kernel), which traces it with all 64 lanes
+ *     (0: never).
  * Results never depend on the schedule (every pixel's operations are the
  * same whichever lanes trace it); only the time does. The defaults are the
  * measured best. A context starts with the defaults. */
@@ -198,6 +203,10 @@ typedef struct rtx_schedule {
     float trace_low;          /* default 0 */
     float trace_medium;       /* default 0 */
     float trace_large;        /* default 0 */
+    float promote_small;      /* default 0; each promote_* in [0, 1e9] */
+    float promote_low;        /* default 0 */
+    float promote_medium;     /* default 500 */
+    float promote_large;      /* default 400 */
     uint32_t tail_coop_max;   /* default 32 */
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
@@ -208,7 +217,8 @@ typedef struct rtx_schedule {
 RTX_API int rtx_schedule_defaults(rtx_schedule *out);
 /* Validates and installs a schedule for later launches of `ctx` (NULL =
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
- * occupancies in (0, 1], trace_* in [0, 0.5], tail_coop_max in 1..64,
+ * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
+ * tail_coop_max in 1..64,
  * priorities in 0..3, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);

@@ -96,6 +96,7 @@ struct rtx_ctx {
     rtx::KTune tune = rtx::default_tune();  // rtx_set_schedule
     hipStream_t aux_stream = nullptr;       // k_trace (tier 1 beside the render), created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    uint64_t epoch = 0;                     // render launches: promotion-queue entry epochs
     double ms_folded = 0.0;         // durations of launches whose pair was recycled
     uint64_t samples = 0;
     uint64_t launches = 0;
@@ -253,6 +254,10 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->trace_low = (float)t.trace_low;
     out->trace_medium = (float)t.trace_medium;
     out->trace_large = (float)t.trace_large;
+    out->promote_small = (float)t.prom_small;
+    out->promote_low = (float)t.prom_low;
+    out->promote_medium = (float)t.prom_medium;
+    out->promote_large = (float)t.prom_large;
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
@@ -280,6 +285,9 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         if (!(o > 0.0f && o <= 1.0f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: occupancies must be in (0, 1]");
     if (s->tail_coop_max < 1 || s->tail_coop_max > 64)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max must be in 1..64");
+    const float pr[] = {s->promote_small, s->promote_low, s->promote_medium, s->promote_large};
+    for (float v : pr)
+        if (!(v >= 0.0f && v <= 1e9f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: promote_* must be in [0, 1e9]");
     const float tr[] = {s->trace_small, s->trace_low, s->trace_medium, s->trace_large};
     for (float v : tr)
         if (!(v >= 0.0f && v <= 0.5f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_* must be in [0, 0.5]");
@@ -305,6 +313,10 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.trace_low = s->trace_low;
     t.trace_medium = s->trace_medium;
     t.trace_large = s->trace_large;
+    t.prom_small = s->promote_small;
+    t.prom_low = s->promote_low;
+    t.prom_medium = s->promote_medium;
+    t.prom_large = s->promote_large;
     t.prio_t1 = s->tier1_priority;
     t.prio_t2 = s->tier2_priority;
     t.prio_hot = s->hot_priority;
@@ -334,6 +346,10 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->trace_low = (float)t.trace_low;
     out->trace_medium = (float)t.trace_medium;
     out->trace_large = (float)t.trace_large;
+    out->promote_small = (float)t.prom_small;
+    out->promote_low = (float)t.prom_low;
+    out->promote_medium = (float)t.prom_medium;
+    out->promote_large = (float)t.prom_large;
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
@@ -484,7 +500,8 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
 
 // Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + 4], then the
 // per-pixel pre-pass state (float4, 16-byte aligned).
-static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 4 + 3) & ~(size_t)3; }
+static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 8 + 3) & ~(size_t)3; }
+constexpr uint32_t kPromCap = 65536;  // promotion queue entries (8 words each)
 
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
@@ -612,7 +629,10 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         c->d_sched = nullptr;
         c->sched_pixels = 0;
         // cost, perm, buckets; then 16-byte aligned per-pixel state
-        RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix) * sizeof(uint32_t)));
+        RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix + 8 * (size_t)kPromCap) * sizeof(uint32_t)));
+        // the promotion queue's epoch words start below every launch's epoch
+        RTX_HIP(hipMemsetAsync(c->d_sched + sched_state_off(npix) + 4 * npix, 0,
+                               8 * (size_t)kPromCap * sizeof(uint32_t), c->stream));
         c->sched_pixels = npix;
     }
     const size_t ps_need = rtx::ps_scratch_floats(p);
@@ -640,6 +660,9 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         RTX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     }
     sched.aux = c->aux_stream;
+    sched.prom_q = c->d_sched + sched_state_off(c->sched_pixels) + 4 * c->sched_pixels;
+    sched.prom_cap = kPromCap;
+    sched.epoch = (uint32_t)++c->epoch;
     sched.ev_fork = c->ev_fork;
     sched.ev_join = c->ev_join;
     hipError_t e = rtx::launch_render(p, sched, c->stream);

@@ -68,6 +68,12 @@ struct KParams {
     uint32_t coop_max;             // queue exhausted: a wave with <= this many pixels traces them in group coop
     uint32_t prio_t1, prio_t2, prio_hot;  // wave priorities (0..3) of tier-1, tier-2 and hot lane-mode waves
     uint32_t trace_ext;            // tier 1 runs in k_trace beside k_render (k_render skips it)
+    // promotion (k_trace beside k_render): once its queue is empty, a lane-mode
+    // wave hands a pixel whose projected remaining segments exceed prom_min
+    // to k_trace at a sample boundary (rtx_kernels.hip, promote)
+    uint32_t *prom;                // [0] entries claimed [1] entries taken [2] pixels written; NULL: off
+    uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
+    uint32_t prom_cap, prom_min, epoch;
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
@@ -90,6 +96,7 @@ struct KTune {
     uint32_t coop_max;                      // KParams::coop_max
     uint32_t prio_t1, prio_t2, prio_hot;    // KParams::prio_*
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
+    double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
 };
 KTune default_tune();
 
@@ -105,6 +112,9 @@ struct KSchedule {
     KTune tune;
     hipStream_t aux;    // k_trace's stream (NULL: tier 1 stays in k_render)
     hipEvent_t ev_fork, ev_join;
+    uint32_t *prom_q;   // promotion queue storage, prom_cap entries of 8 words
+    uint32_t prom_cap;
+    uint32_t epoch;     // launch counter: a promotion entry is ready when its last word equals it
 };
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)

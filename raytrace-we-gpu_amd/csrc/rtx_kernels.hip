@@ -96,6 +96,11 @@ constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (defaul
 // 16.2-16.6 with 20 %; 20.3 both; 30.7 vs 44 with 5 %: its few waves queue the many medium-share
 // tier-1 pixels), so it is off there; the whole frame is R3i.
 constexpr double kTraceSmall = 0.0, kTraceLow = 0.0, kTraceMedium = 0.0, kTraceLarge = 0.0;
+// promotion thresholds (projected further segments; 0: off): a whole frame
+// 50.0 -> 46.5 ms at 300-500 (700: 48.5, 1000: 49-51); a 2-way split
+// 30.6-31.1 -> 29.6-30.0 ms at 250-500; 4- and 8-way splits 1-2 ms slower
+// at any threshold
+constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLarge = 400.0;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -1010,11 +1015,55 @@ __device__ __forceinline__ int path_segment(const KParams &P, LaneT &L, int hit,
     return path_segment_m<false>(P, L, hit, t, M, ScatterSpec{}, sky_col);
 }
 
+// Cross-XCD hand-off without cache maintenance. On gfx950 an agent-scope
+// release writes back the issuing XCD's L2 (buffer_wbl2) and an acquire
+// invalidates it (buffer_inv): issued per iteration they evict the scene and
+// queue lines of every k_render wave on that XCD (parts 8 with promotion on:
+// 15 -> 38 ms). Relaxed agent-scope loads and stores are already
+// coherent across XCDs (sc1: they bypass the non-coherent L2 state), so the
+// hand-off only needs the stores to complete in order: wait for every
+// outstanding vector-memory operation (vmcnt 0) before the flag store, and
+// keep the compiler from moving atomics across the wait.
+__device__ __forceinline__ void agent_store_order() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt unconstrained (gfx9 encoding)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Promotion (KParams::prom): once the queue is exhausted, a lane whose pixel
+// is projected, at a sample boundary, to need more than prom_min further
+// segments (its own rate so far in this launch times the samples left) hands
+// the pixel's state (gid, sample, seed, acc) to the promotion queue and goes
+// idle; a wave with nothing else to do (an idle k_render wave, or k_trace
+// after tier 1) traces the rest of the pixel with all its lanes. Entries are
+// published with agent-scope atomics (the consumer may sit on another XCD,
+// whose L2 does not see these stores otherwise): the fields, a wait for their
+// completion, then the epoch word (agent_store_order).
+__device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
+    const uint32_t done = L.sample - P.cost_spp;  // samples traced in this launch (>= 1 here)
+    const uint32_t segs = L.segs - L.seg0;
+    if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
+    const uint32_t slot = atomicAdd(&P.prom[0], 1u);
+    if (slot >= P.prom_cap) return false;  // queue full: the lane keeps its pixel
+    uint32_t *e = P.prom_q + 8u * slot;
+    __hip_atomic_store(e + 0, L.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e + 1, L.sample, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e + 2, __float_as_uint(L.seed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e + 3, __float_as_uint(L.acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e + 4, __float_as_uint(L.acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e + 5, __float_as_uint(L.acc.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    agent_store_order();
+    __hip_atomic_store(e + 7, P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 // Chain-RNG lane: one segment, then the pixel's next sample when the path
 // ends (acc += colour in sample order, :269-284), or the pixel's output
-// after its last sample (clears `active`).
+// after its last sample (clears `active`). may_promote: the wave's queue is
+// exhausted and promotion is on. Returns true when the pixel was promoted.
 template <bool kCost = false>
-__device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L, int hit, float t) {
+__device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L, int hit, float t,
+                                      bool may_promote = false) {
     L.segs++;
     f3 c;
     const int r = path_segment(P, L, hit, t, c);
@@ -1026,10 +1075,14 @@ __device__ __forceinline__ void shade(const KParams &P, const Frame &F, Lane &L,
             write_pixel<kCost>(P, L);
             L.active = false;
             diag_pixel_end(P, L.gid);
+        } else if (!kCost && may_promote && promote(P, L)) {
+            L.active = false;  // the promotion queue owns the pixel now
+            return true;
         } else {
             begin_sample(P, F, L.x, L.y, L);
         }
     }
+    return false;
 }
 
 __device__ __forceinline__ void lane_pixel(const KParams &P, uint32_t gid, uint32_t &x, uint32_t &y) {
@@ -1270,6 +1323,55 @@ __device__ __forceinline__ void trace_pixel_uniform(const KParams &P, const Fram
     RTX_CP(3)
 }
 
+// Promotion queue service: wait for an entry and load it into W (every lane
+// the same state, at the entry's sample boundary), or return false once every
+// pixel of the launch is written (prom[2], counted by the writers: k_render
+// waves when they go idle, k_trace per pixel) — promoted pixels are counted
+// by whoever finishes them, so the count reaches npix only when the queue
+// holds nothing more. The tail is read after the count: a pixel is promoted
+// (slot claimed, entry stored) before its old wave can go idle and flush.
+// All relaxed (agent_store_order). Polls sleep ~8k clocks at priority 0;
+// safety valve: a wave that finds nothing for 2 s leaves (a bug would then
+// show as unwritten pixels, never as a hung GPU).
+__device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, uint32_t npix, Lane &W) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_setprio(0);
+    for (;;) {
+        const uint32_t done = __hip_atomic_load(&P.prom[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done >= npix) return false;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const uint32_t t = min(__hip_atomic_load(&P.prom[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.prom_cap);
+        const uint32_t h = __hip_atomic_load(&P.prom[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t got = ~0u;
+        if (h < t && (threadIdx.x & 63u) == 0u) got = atomicCAS(&P.prom[1], h, h + 1u) == h ? h : ~0u;
+        got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
+        if (got != ~0u) {
+            const uint32_t *e = P.prom_q + 8u * got;
+            while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;  // 2 s at 100 MHz
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the fields are read after the epoch matched
+            W.gid = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            W.sample = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            W.seed = __uint_as_float(__hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            W.acc = mk3(__uint_as_float(__hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                        __uint_as_float(__hip_atomic_load(e + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                        __uint_as_float(__hip_atomic_load(e + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            if (W.gid >= npix || W.sample >= P.spp) return false;  // never: a torn entry ends the wave, not the GPU
+            lane_pixel(P, W.gid, W.x, W.y);
+            W.seg0 = W.segs;
+            W.slot = ~0u;
+            W.active = true;
+            begin_sample(P, F, W.x, W.y, W);
+            diag_pixel_start(P, W.gid, 3ull);
+            return true;
+        }
+        if (h >= t) __builtin_amdgcn_s_sleep(127);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;
+    }
+}
+
 // Render kernel (chain RNG), per-wave independent; sphere blocks are read
 // with scalar loads (a block-wide LDS copy serves the coop and the resolve of
 // scenes up to kCoopLds spheres). kPersist: the grid holds as many waves as the GPU keeps resident and
@@ -1290,12 +1392,12 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
-    if (coop_lds) {
-        __syncthreads();
-    } else if (kPF) {
-        if (threadIdx.x == 0) *pack = 0u;
-        __syncthreads();
-    }
+    // promotion: the block's first wave to go idle serves the queue, the others leave
+    __shared__ uint32_t s_server;
+    const bool prom_on = kPersist && !kCost && P.prom != nullptr;
+    if (kPF && threadIdx.x == 0) *pack = 0u;
+    if (prom_on && threadIdx.x == 0) s_server = 0u;
+    if (coop_lds || kPF || prom_on) __syncthreads();
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
@@ -1317,6 +1419,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
+    uint32_t written = 0;  // pixels this wave wrote since it last reported (promotion's exit count)
     Diag D;
     D.begin();
     for (;;) {
@@ -1326,7 +1429,21 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
         const uint64_t act = __ballot(L.active);
         D.section(0);
-        if (act == 0ull) break;  // spp, depth > 0: idle after both queues => drained
+        if (act == 0ull) {  // spp, depth > 0: idle after both queues => drained
+            if (!prom_on) break;
+            if (written != 0u && (threadIdx.x & 63u) == 0u)
+                __hip_atomic_fetch_add(&P.prom[2], written, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            written = 0;
+            uint32_t srv = 0;
+            if ((threadIdx.x & 63u) == 0u) srv = atomicCAS(&s_server, 0u, threadIdx.x / 64u + 1u);
+            srv = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)srv, 0, 64));
+            if (srv != 0u && srv != threadIdx.x / 64u + 1u) break;  // another wave serves this block
+            if (!take_promoted(P, F, npix, L)) break;
+            L.active = (threadIdx.x & 63u) == 0u;  // one ray, traced by the whole wave (tier-1 coop)
+            H.tier = 1;
+            continue;
+        }
+        const uint64_t was_active = act;
         D.iteration(act);
         if (heavy || (exhausted && (uint32_t)__popcll(act) <= P.coop_max)) {
             D.tail_iteration();
@@ -1338,6 +1455,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             set_prio(H.tier == 1u ? P.prio_t1 : H.tier == 2u ? P.prio_t2 : (uint32_t)kTailPrio);
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
+            bool promoted = false;
             int my_hit = coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
                                                      coop_ws, my_best, my_seq, cp, ctqp)
                                   : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
@@ -1347,8 +1465,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                     my_best = __uint_as_float(0x7f800000u);
                     my_hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
-                shade<kCost>(P, F, L, min(my_hit, last), my_best);
+                // the tail's pixels may be promoted (tier-1 waves already
+                // trace one ray with every lane; promoting tier-2 pixels
+                // measured 1-6 ms slower at R = 2, 4, 8: profiles/R3r_*)
+                promoted = shade<kCost>(P, F, L, min(my_hit, last), my_best, prom_on && exhausted && H.tier == 0u);
             }
+            if (prom_on)
+                written += (uint32_t)__popcll(act & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
             D.coop_end(cp, H.tier);
             if (H.tier == 0u) __builtin_amdgcn_s_setprio(0);  // a heavy wave keeps its priority
             D.section(3);
@@ -1358,6 +1481,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
         set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
+        bool promoted = false;
         if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
@@ -1368,9 +1492,11 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
-            shade<kCost>(P, F, L, min(hit, last), best);
+            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
         }
         D.section(2);
+        if (prom_on)  // pixels written this iteration (promoted ones are counted by whoever finishes them)
+            written += (uint32_t)__popcll(was_active & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
     }
     D.finish(P);
     count_segments(P, L.segs);
@@ -1412,8 +1538,25 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
         if (threadIdx.x == 0) {
             write_pixel<false>(P, W);
             diag_pixel_end(P, W.gid);
+            if (P.prom) __hip_atomic_fetch_add(&P.prom[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         segs += W.segs;
+    }
+    // then the promotion queue, until every pixel of the launch is written
+    if (P.prom) {
+        Lane W;
+        W.segs = 0;
+        while (take_promoted(P, F, npix, W)) {
+            const uint32_t s0 = W.segs;
+            set_prio(P.prio_t1);
+            trace_pixel_uniform(P, F, sl, W, nullptr, nullptr);
+            if (threadIdx.x == 0) {
+                write_pixel<false>(P, W);
+                diag_pixel_end(P, W.gid);
+                __hip_atomic_fetch_add(&P.prom[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            segs += W.segs - s0;
+        }
     }
     if (threadIdx.x == 0 && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
 }
@@ -1528,6 +1671,10 @@ KTune default_tune() {
     t.trace_low = kTraceLow;
     t.trace_medium = kTraceMedium;
     t.trace_large = kTraceLarge;
+    t.prom_small = kPromSmall;
+    t.prom_low = kPromLow;
+    t.prom_medium = kPromMedium;
+    t.prom_large = kPromLarge;
     return t;
 }
 namespace {
@@ -2023,7 +2170,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     c.perm = nullptr;  // index order
     c.heavy = nullptr;
     c.prio_slots = 0;
-    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 4) * sizeof(uint32_t), stream);
+    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 8) * sizeof(uint32_t), stream);
     if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (pf) {
@@ -2069,6 +2216,20 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         const double frac = px_per_lane < tune.rho ? tune.trace_small : px_per_lane < tune.rho_low ? tune.trace_low
                             : px_per_lane < tune.rho2 ? tune.trace_medium : tune.trace_large;
         trace_waves = (uint32_t)(frac * blocks * (kRB / 64) + 0.5);
+    }
+    // promotion (any scene): served by idle k_render waves, and by k_trace
+    // after tier 1 when it runs
+    {
+        const double px_per_lane = (double)lanes / ((double)blocks * kRB);
+        const double pm = px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
+                          : px_per_lane < tune.rho2 ? tune.prom_medium : tune.prom_large;
+        if (pm > 0.0 && sched.prom_q && sched.prom_cap > 0) {
+            q.prom = sched.buckets + 2 * kCostBuckets + 4;  // zeroed with the buckets
+            q.prom_q = sched.prom_q;
+            q.prom_cap = sched.prom_cap;
+            q.prom_min = (uint32_t)std::min<double>(pm, 4e9);
+            q.epoch = sched.epoch;
+        }
     }
     if (trace_waves > 0) {
         q.trace_ext = 1u;

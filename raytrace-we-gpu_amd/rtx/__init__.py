@@ -60,7 +60,8 @@ class rtx_schedule(C.Structure):
                 ("low_share", C.c_float), ("medium_share", C.c_float), ("hot_fraction", C.c_float),
                 ("occupancy_small", C.c_float), ("occupancy_low", C.c_float), ("occupancy_normal", C.c_float),
                 ("trace_small", C.c_float), ("trace_low", C.c_float), ("trace_medium", C.c_float),
-                ("trace_large", C.c_float),
+                ("trace_large", C.c_float), ("promote_small", C.c_float), ("promote_low", C.c_float),
+                ("promote_medium", C.c_float), ("promote_large", C.c_float),
                 ("tail_coop_max", C.c_uint32), ("tier1_priority", C.c_uint32), ("tier2_priority", C.c_uint32),
                 ("hot_priority", C.c_uint32), ("reserved", C.c_uint32)]
 

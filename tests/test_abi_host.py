@@ -110,6 +110,7 @@ def test_schedule_defaults_and_validation(rtx):
     assert d.tier2_bar == pytest.approx(1e30)
     assert (d.tier1_priority, d.tier2_priority, d.hot_priority) == (3, 2, 3)
     assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == (0.0, 0.0, 0.0, 0.0)
+    assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (0.0, 0.0, 500.0, 400.0)
     assert d.occupancy_small == d.occupancy_low == d.occupancy_normal == 1.0
     lib = rtx.load_library()
     assert lib.rtx_set_schedule(None, C.byref(d)) == -1

@@ -772,7 +772,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})
@@ -804,6 +804,43 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
             want, _ = oracle.render_rows(world, frame, rows, nthreads=8)
             assert_bits_equal(got, want, f"schedule {ex}, part {part} of {nparts}")
     gpu_ctx.set_schedule()
+
+
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
+    """Tier 1 in k_trace beside k_render, and promotion: once its queue is
+    empty a lane hands its pixel to k_trace at a sample boundary (threshold 1
+    projected segment: nearly every pixel still in flight is handed over,
+    the 65,536-entry queue overflows on the whole frame and lanes keep the
+    rest). Whole frames and row-tile shares of every size class, against the
+    oracle bit for bit, and the frame's segment count."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(11, depth=50, spp=12)
+    W, H, T = 320, 180, 5
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    want_all, segs_all = oracle.render_rows(world, frame, np.arange(H), nthreads=8)
+    for sched in (dict(trace_small=0.3, trace_low=0.3, trace_medium=0.3, trace_large=0.3, tier1_bar=1.2,
+                       tier1_bar_small=1.5, tier1_bar_low=1.5),
+                  dict(trace_small=0.3, trace_low=0.3, trace_medium=0.3, trace_large=0.3, promote_small=1,
+                       promote_low=1, promote_medium=1, promote_large=1),
+                  dict(trace_small=0.05, trace_low=0.05, trace_medium=0.05, trace_large=0.05, promote_small=50,
+                       promote_low=50, promote_medium=50, promote_large=50, tier1_bar=1.3)):
+        ctx.set_schedule()
+        ctx.set_schedule(**sched)
+        for nparts, part in ((1, 0), (2, 1), (4, 3), (8, 2)):
+            rows = rtx.part_row_ids(H, T, part, nparts)
+            buf = ctx.alloc((len(rows), W, 4))
+            ctx.stats_reset()
+            ctx.render_rows(T, part, nparts, buf.ptr)
+            st = ctx.stats()
+            got = buf.numpy()
+            buf.free()
+            assert_bits_equal(got, want_all[rows], f"{ctx_name} {sched} part {part} of {nparts}")
+            if nparts == 1:
+                assert st.segments == segs_all
+    ctx.set_schedule()
 
 
 def test_progressive_accumulation_bit_exact(gpu_ctx, oracle, rtx):

@@ -5,7 +5,8 @@ SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a
          "a2m": "tier2_bar_medium", "a2": "tier2_bar", "rho": "small_share", "rhol": "low_share", "rho2": "medium_share",
          "prio": "hot_fraction", "occs": "occupancy_small", "occl": "occupancy_low", "occn": "occupancy_normal",
          "coop": "tail_coop_max", "p1": "tier1_priority", "trs": "trace_small", "trl": "trace_low",
-         "trm": "trace_medium", "trL": "trace_large", "p2": "tier2_priority", "ph": "hot_priority"}
+         "trm": "trace_medium", "trL": "trace_large", "prs": "promote_small", "prl": "promote_low",
+         "prm": "promote_medium", "prL": "promote_large", "p2": "tier2_priority", "ph": "hot_priority"}
 
 
 def schedule_of(setting):
