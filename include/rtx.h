@@ -173,6 +173,8 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     low / larger part;
  *   - tail_coop_max: once the queue is empty a wave with at most this many
  *     pixels left traces them with several lanes per ray (1..64);
+ *     tail_coop_max_large for scenes above 640 spheres (no LDS copy of the
+ *     scene: the group's sphere reads go to L2/HBM);
  *   - trace_*: for scenes up to 640 spheres tier 1 runs in its own kernel
  *     beside the render (one pixel per wave, all 64 lanes on its ray), with
  *     this fraction of the resident waves for a small / low / medium /
@@ -208,6 +210,7 @@ typedef struct rtx_schedule {
     float promote_medium;     /* default 500 */
     float promote_large;      /* default 400 */
     uint32_t tail_coop_max;   /* default 32 */
+    uint32_t tail_coop_max_large; /* default 8: the same for scenes above 640 spheres */
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
@@ -218,7 +221,7 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
 /* Validates and installs a schedule for later launches of `ctx` (NULL =
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
- * tail_coop_max in 1..64,
+ * tail_coop_max and tail_coop_max_large in 1..64,
  * priorities in 0..3, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);

@@ -250,6 +250,7 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->occupancy_low = (float)t.occ_low;
     out->occupancy_normal = (float)t.occ_normal;
     out->tail_coop_max = t.coop_max;
+    out->tail_coop_max_large = t.coop_max_large;
     out->trace_small = (float)t.trace_small;
     out->trace_low = (float)t.trace_low;
     out->trace_medium = (float)t.trace_medium;
@@ -285,6 +286,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         if (!(o > 0.0f && o <= 1.0f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: occupancies must be in (0, 1]");
     if (s->tail_coop_max < 1 || s->tail_coop_max > 64)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max must be in 1..64");
+    if (s->tail_coop_max_large < 1 || s->tail_coop_max_large > 64)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max_large must be in 1..64");
     const float pr[] = {s->promote_small, s->promote_low, s->promote_medium, s->promote_large};
     for (float v : pr)
         if (!(v >= 0.0f && v <= 1e9f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: promote_* must be in [0, 1e9]");
@@ -309,6 +312,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.occ_low = s->occupancy_low;
     t.occ_normal = s->occupancy_normal;
     t.coop_max = s->tail_coop_max;
+    t.coop_max_large = s->tail_coop_max_large;
     t.trace_small = s->trace_small;
     t.trace_low = s->trace_low;
     t.trace_medium = s->trace_medium;
@@ -342,6 +346,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->occupancy_low = (float)t.occ_low;
     out->occupancy_normal = (float)t.occ_normal;
     out->tail_coop_max = t.coop_max;
+    out->tail_coop_max_large = t.coop_max_large;
     out->trace_small = (float)t.trace_small;
     out->trace_low = (float)t.trace_low;
     out->trace_medium = (float)t.trace_medium;

@@ -93,7 +93,8 @@ struct KParams {
 struct KTune {
     double a1, a1_small, a1_low, a2_small, a2_medium, a2_large, rho, rho_low, rho2, prio_frac;
     double occ_small, occ_low, occ_normal;  // fraction of the resident waves launched for a small / low / larger share
-    uint32_t coop_max;                      // KParams::coop_max
+    uint32_t coop_max;                      // KParams::coop_max (scenes with the coop's LDS copy)
+    uint32_t coop_max_large;                // ... and without it (n > kCoopLds)
     uint32_t prio_t1, prio_t2, prio_hot;    // KParams::prio_*
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)

@@ -79,6 +79,7 @@ __device__ __forceinline__ float dir_len2(f3 d) { return fmaf(d.z, d.z, fmaf(d.y
 // are also set by the stress build. Everything else is a fixed product
 // constant.
 constexpr int kCoopMax = 32;            // tail mode: a wave with <= this many active lanes traces their rays together
+constexpr int kCoopMaxLarge = 8;       // the same above kCoopLds spheres: 32 made C5 1.86 -> 2.40 s (group reads from L2/HBM)
                                         // (8 -> 32 with the sphere-pair coop: parts 1/4/8 -0.8..1.5 ms, R3e)
 constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wave
 constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
@@ -247,6 +248,10 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 // per-ray ku/kv of rtx_prefilter.h line_test_flat) or not (the 7-op test,
 // k0/k1 = nou/nov). Returns the block to resume at; `full` when it stopped
 // because some lane's list is full.
+#ifndef RTX_PF_LDS  // A/B build: large scenes stream through a per-wave LDS tile (below)
+#define RTX_PF_LDS 0
+#endif
+constexpr uint32_t kPfLdsBytes = RTX_PF_LDS ? (kRB / 64) * 64 * 16 : 0;  // 1 KiB per wave
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
 #define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
 #endif
@@ -301,7 +306,40 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
         return false;
     };
     full = true;
-    if constexpr (kPF) {
+    if constexpr (kPF && RTX_PF_LDS) {
+        // A/B build: the scene streams through a per-wave
+        // LDS tile of 8 blocks (1 KiB: one coalesced 16-byte load per lane,
+        // the next tile's loads in flight while this one is scanned), and
+        // each block is read from it with 8 broadcast ds_read_b128 into VGPRs.
+        float4 *tl = const_cast<float4 *>(reinterpret_cast<const float4 *>(lds_pr)) + 64u * ((threadIdx.x & 255u) >> 6);
+        const float4 *gp = (const float4 *)(const float *)pre;
+        const uint32_t lane = threadIdx.x & 63u;
+        auto fetch = [&](uint32_t tb) { return gp[8u * min(tb + (lane >> 3), end - 1u) + (lane & 7u)]; };
+        uint32_t tb = b & ~7u;
+        float4 cur = fetch(tb);
+        for (;;) {
+            __builtin_amdgcn_wave_barrier();
+            tl[lane] = cur;
+            __builtin_amdgcn_wave_barrier();
+            const bool more = tb + 8u < end;
+            if (more) cur = fetch(tb + 8u);
+            const uint32_t e = min(tb + 8u, end);
+            for (; b < e; ++b) {
+                const float4 *q = tl + 8u * (b - tb);
+                float4 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = q[t];
+                auto blk = [&](int i) {
+                    const float4 w = v[i >> 2];
+                    const int c = i & 3;
+                    return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
+                };
+                if (step(blk, b)) return b + 1;
+            }
+            if (!more) break;
+            tb += 8u;
+        }
+    } else if constexpr (kPF) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
         f16v a_lo, a_hi, b_lo, b_hi;
         sload_blk(pre + 32 * b, a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
@@ -846,6 +884,9 @@ __device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 
     P.out[gid] = o;
 }
 
+#ifndef RTX_EXTRA_BYTES
+#define RTX_EXTRA_BYTES 0
+#endif
 // A pixel's output (output_pixel), or the scheduling pre-pass's record of it.
 template <bool kCost = false>
 __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
@@ -856,6 +897,10 @@ __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
         return;
     }
     output_pixel(P, L.gid, L.acc);
+    // A/B build (HBM traffic): the pixel's final state also
+    // goes back to its (dead) resume slot: +16 B per pixel of the same
+    // scattered cost-order stores as the image
+    if (RTX_EXTRA_BYTES && P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
 }
 
 // Diffuse direction before normalisation, target - p (ShaderCompute.hlsl:
@@ -1392,6 +1437,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
+    const float *pf_tile = kPF && RTX_PF_LDS ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
     // promotion: the block's first wave to go idle serves the queue, the others leave
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
@@ -1490,7 +1536,10 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                 ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
                                                         L.a, L.inv_a, kTMin, best, list, nullptr, 0,
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
-                                : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
+                                : RTX_PF_LDS && kPF
+                                      ? hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o,
+                                                              L.d, L.a, L.inv_a, kTMin, best, list, nullptr, 0, pf_tile)
+                                      : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
             promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
         }
@@ -1664,6 +1713,7 @@ KTune default_tune() {
     t.prio_frac = kPrioFracX100 / 100.0;
     t.occ_small = t.occ_low = t.occ_normal = 1.0;
     t.coop_max = (uint32_t)kCoopMax;
+    t.coop_max_large = (uint32_t)kCoopMaxLarge;
     t.prio_t1 = 3;
     t.prio_t2 = 2;
     t.prio_hot = 3;
@@ -1728,6 +1778,9 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
 // and a wave has at most kCoopMax samples left, it traces them with the
 // group coop of the chain kernel (several lanes per ray), at a raised wave
 // priority: the frame's last, longest paths end sooner.
+#ifndef RTX_PS_ITEM_MAJOR  // per-sample scratch layout: 1 = item-major (37.6 vs 38.5 ms, 8.8 vs 13.5 GB per C2 frame: R3u), 0 = sample-major
+#define RTX_PS_ITEM_MAJOR 1
+#endif
 constexpr int kPsSlots = 4;
 constexpr uint32_t kPsStateBytes = (kRB / 64) * kPsSlots * 4 * sizeof(uint32_t);  // per block
 struct PsLane {
@@ -1755,7 +1808,7 @@ __device__ __forceinline__ void ps_start(const KParams &P, const Frame &F, uint3
     L.col = mk3(1.0f, 1.0f, 1.0f);
     L.bounce = 0;
     L.slot = slot;
-    L.sidx = s * npx + po;
+    L.sidx = RTX_PS_ITEM_MAJOR ? item : s * npx + po;
     L.active = true;
 }
 
@@ -1770,15 +1823,20 @@ __device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t
     if (po >= npx) return;
     f3 acc = mk3(0.0f, 0.0f, 0.0f);
     uint32_t s = 0;
+    // sample s of pixel po: [s * npx + po] (sample-major), or [po * spp + s]
+    // (item-major: the order the lanes take the items in)
+    const uint32_t ss = RTX_PS_ITEM_MAJOR ? 1u : npx;
+    if (RTX_PS_ITEM_MAJOR) c += po * P.spp;
+    else c += po;
     for (; s + 8 <= P.spp; s += 8) {  // eight samples' loads in flight, adds in order
         float4 v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = c[(s + k) * npx + po];
+        for (int k = 0; k < 8; ++k) v[k] = c[(s + k) * ss];
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = acc + mk3(v[k].x, v[k].y, v[k].z);
     }
     for (; s < P.spp; ++s) {
-        const float4 v = c[s * npx + po];
+        const float4 v = c[s * ss];
         acc = acc + mk3(v.x, v.y, v.z);
     }
     output_pixel(P, px0 + po, acc);
@@ -2062,7 +2120,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() + 16 : kListBytes) + kCoopBytes +  // kPF: the pack word
+    return (use_pf(s) ? list_bytes<true>() + 16 + kPfLdsBytes : kListBytes) + kCoopBytes +  // kPF: the pack word
            (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
@@ -2133,7 +2191,7 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
 hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
     const KTune &tune = sched.tune;  // validated by rtx_set_schedule
     KParams p = p_in;
-    p.coop_max = min(max(tune.coop_max, 1u), 64u);
+    p.coop_max = min(max(p.scene.n <= kCoopLds ? tune.coop_max : tune.coop_max_large, 1u), 64u);
     p.prio_t1 = tune.prio_t1;
     p.prio_t2 = tune.prio_t2;
     p.prio_hot = tune.prio_hot;
@@ -2217,9 +2275,11 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
                             : px_per_lane < tune.rho2 ? tune.trace_medium : tune.trace_large;
         trace_waves = (uint32_t)(frac * blocks * (kRB / 64) + 0.5);
     }
-    // promotion (any scene): served by idle k_render waves, and by k_trace
-    // after tier 1 when it runs
-    {
+    // promotion: served by idle k_render waves, and by k_trace after tier 1
+    // when it runs. Scenes with the coop's LDS copy only: at 100k spheres a
+    // one-ray wave reads the scene from L2/HBM and is slower than lane mode
+    // (C5 1.86 -> 2.39 s with promotion)
+    if (!pf && p.scene.n <= kCoopLds) {
         const double px_per_lane = (double)lanes / ((double)blocks * kRB);
         const double pm = px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
                           : px_per_lane < tune.rho2 ? tune.prom_medium : tune.prom_large;
