@@ -530,10 +530,15 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 template <bool kPF, typename Ld>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
                                                 float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
-                                                uint32_t start = 0, const float *lds_pr = nullptr) {
+                                                uint32_t start = 0, const float *lds_pr = nullptr,
+                                                bool live = true) {
     const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
-    const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    if (!live) {  // a lane without a ray (RTX_PF_LDS: every lane fills the tile): nothing is flagged
+        T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
+        T.thr = __uint_as_float(0x7f800000u);
+    }
     const float best0 = best;
     int idx = -1;
     bool ok = true;
@@ -834,6 +839,9 @@ struct Lane {
     uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
     uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments)
     bool active;         // tracing a pixel
+#if RTX_CHUNK
+    uint32_t cb, ce;     // the wave's private run of queue slots (refill, A/B build)
+#endif
 };
 
 __device__ __forceinline__ void set_dir(Lane &L, f3 d) {
@@ -1193,10 +1201,54 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 // slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
 // per refill (ballot + lane rank). Returns true once the queue is
 // exhausted (wave-uniform).
+#ifndef RTX_CHUNK  // A/B build: private runs of queue slots per wave (refill)
+#define RTX_CHUNK 0
+#endif
+#ifndef RTX_REFILL_MIN  // A/B build: a wave with live lanes refills only once this many are idle
+#define RTX_REFILL_MIN 1  // (consecutive queue slots for more of its lanes: coherence vs idle lanes)
+#endif
 __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_t lo, uint32_t hi, Lane &L) {
     const uint64_t idle = __ballot(!L.active);
     if (idle == 0ull) return false;
     const uint32_t cnt = (uint32_t)__popcll(idle);
+    if (RTX_REFILL_MIN > 1 && cnt < RTX_REFILL_MIN && cnt < 64u) return false;
+#if RTX_CHUNK
+    // A/B build: the wave's idle lanes take consecutive slots of a private
+    // run [cb, ce) of the queue, which is re-stocked RTX_CHUNK slots at a
+    // time, so that its lanes hold pixels from few runs of the cost order
+    // (coherent rays) instead of one slot per refill from wherever the queue
+    // head is. Off for the last eighth of the queue (no pixel waits in a
+    // busy wave's run while other waves are idle).
+    {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+        const uint32_t avail = L.ce - L.cb;
+        uint32_t nb = 0, n = 0;
+        if (cnt > avail) {
+            n = cnt - avail;
+            if (L.cb < hi - (hi - lo) / 8u) n = max(n, (uint32_t)RTX_CHUNK);
+            if (lane == 0u) nb = atomicAdd(P.queue, n);
+            nb = lo + (uint32_t)__shfl((int)nb, 0, 64);
+        }
+        if (!L.active) {
+            const uint32_t g = rank < avail ? L.cb + rank : nb + (rank - avail);
+            if (g < hi) {
+                start_pixel(P, F, P.perm ? P.perm[g] : g, L);
+                L.slot = g;
+                diag_pixel_start(P, L.gid, 0);
+            }
+        }
+        if (cnt > avail) {
+            L.cb = nb + (cnt - avail);
+            L.ce = nb + n;
+            if (L.cb >= hi) return true;
+            L.ce = min(L.ce, hi);
+        } else {
+            L.cb += cnt;
+        }
+        return false;
+    }
+#endif
     const int leader = __ffsll((long long)idle) - 1;
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t base = 0;
@@ -1452,6 +1504,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     L.active = false;
     L.segs = 0;
     L.slot = ~0u;
+#if RTX_CHUNK
+    L.cb = L.ce = 0u;
+#endif
     bool exhausted = !kPersist;
     if (!kPersist) {
         const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
@@ -1528,7 +1583,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // so its time per segment is not stretched by the SIMD's other waves
         set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
         bool promoted = false;
-        if (L.active) {
+        if (RTX_PF_LDS && kPF) {  // A/B build: every lane of the wave fills the scan's LDS tile
+            float best = __uint_as_float(0x7f800000u);
+            const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
+                                                  L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
+            D.section(1);
+            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
+        } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
             // from it (the same centre and radius floats as cen) instead of HBM/L2
@@ -1536,10 +1597,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                 ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
                                                         L.a, L.inv_a, kTMin, best, list, nullptr, 0,
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
-                                : RTX_PF_LDS && kPF
-                                      ? hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o,
-                                                              L.d, L.a, L.inv_a, kTMin, best, list, nullptr, 0, pf_tile)
-                                      : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
+                                : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
             promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
         }

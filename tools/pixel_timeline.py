@@ -2,7 +2,7 @@
 """Per-pixel timeline of one rank's share of the C2 frame (diagnostic; needs
 the RTX_DIAG_PIXEL build, lib/variants/librtx_ptime.so). For every pixel of
 rtx_render_rows(T, part, R): its start time and queue (0 lane mode, 1 tier-1
-heavy, 2 tier-2 heavy), its end time, and its segment count
+heavy, 2 tier-2 heavy, 3 promoted), its end time, and its segment count
 (rtx_debug_pixel_cost). Shows what ends the part: which pixels finish last,
 how they were traced and their time per segment.
 
@@ -24,10 +24,13 @@ ap.add_argument("--parts", type=int, nargs="*", default=[1, 2, 8])
 ap.add_argument("--which", type=int, default=0, help="part index to trace (mod R)")
 ap.add_argument("--tile-rows", type=int, default=5)
 ap.add_argument("--set", default="", help="schedule fields (tools/heavy_sweep.py syntax), e.g. a1=1.5,coop=32")
+ap.add_argument("--grid", type=int, default=11, help="random_world grid (159 with --cap 100000: C5)")
+ap.add_argument("--cap", type=int, default=0)
+ap.add_argument("--spp", type=int, default=100)
 a = ap.parse_args()
 
 W, H, T = 1920, 1080, a.tile_rows
-world = rtx.random_world(11, depth=50, spp=100)
+world = rtx.random_world(a.grid, capacity=a.cap or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
 ctx = rtx.Context(0, lib=rtx.load_library(a.lib))
 if a.set:
@@ -65,7 +68,7 @@ for R in a.parts:
     last = np.argsort(-e_us)[:12]
     heavy = np.argsort(-seg)[:12]
     modes = {}
-    for m in (0, 1, 2):
+    for m in (0, 1, 2, 3):  # 3: promoted (start = the promotion)
         sel = ok & (mode == m)
         if sel.any():
             modes[str(m)] = {"pixels": int(sel.sum()), "segments_mean": round(float(seg[sel].mean()), 1),
