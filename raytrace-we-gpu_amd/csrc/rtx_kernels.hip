@@ -251,7 +251,7 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 #ifndef RTX_PF_LDS  // A/B build: large scenes stream through a per-wave LDS tile (below)
 #define RTX_PF_LDS 0
 #endif
-constexpr uint32_t kPfLdsBytes = RTX_PF_LDS ? (kRB / 64) * 64 * 16 : 0;  // 1 KiB per wave
+constexpr uint32_t kPfLdsBytes = (kRB / 64) * 64 * 16 * RTX_PF_LDS;  // RTX_PF_LDS KiB per wave
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
 #define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
 #endif
@@ -308,22 +308,34 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
     full = true;
     if constexpr (kPF && RTX_PF_LDS) {
         // A/B build: the scene streams through a per-wave
-        // LDS tile of 8 blocks (1 KiB: one coalesced 16-byte load per lane,
-        // the next tile's loads in flight while this one is scanned), and
-        // each block is read from it with 8 broadcast ds_read_b128 into VGPRs.
-        float4 *tl = const_cast<float4 *>(reinterpret_cast<const float4 *>(lds_pr)) + 64u * ((threadIdx.x & 255u) >> 6);
+        // LDS tile of 8 * RTX_PF_LDS blocks (RTX_PF_LDS KiB: coalesced 16-byte
+        // loads, one per lane per KiB, the next tile's loads in flight while
+        // this one is scanned), and each block is read from it with 8
+        // broadcast ds_read_b128 into VGPRs. Every lane of the wave runs this
+        // (hit_world_pre_ld's `live`).
+        constexpr uint32_t kT = 8u * RTX_PF_LDS;  // blocks per tile
+        float4 *tl = const_cast<float4 *>(reinterpret_cast<const float4 *>(lds_pr)) +
+                     64u * RTX_PF_LDS * ((threadIdx.x & 255u) >> 6);
         const float4 *gp = (const float4 *)(const float *)pre;
         const uint32_t lane = threadIdx.x & 63u;
-        auto fetch = [&](uint32_t tb) { return gp[8u * min(tb + (lane >> 3), end - 1u) + (lane & 7u)]; };
-        uint32_t tb = b & ~7u;
-        float4 cur = fetch(tb);
+        auto fetch = [&](uint32_t tb, uint32_t k) {
+            return gp[8u * min(tb + 8u * k + (lane >> 3), end - 1u) + (lane & 7u)];
+        };
+        uint32_t tb = b - b % kT;
+        float4 cur[RTX_PF_LDS ? RTX_PF_LDS : 1];
+#pragma unroll
+        for (uint32_t k = 0; k < RTX_PF_LDS; ++k) cur[k] = fetch(tb, k);
         for (;;) {
             __builtin_amdgcn_wave_barrier();
-            tl[lane] = cur;
+#pragma unroll
+            for (uint32_t k = 0; k < RTX_PF_LDS; ++k) tl[64u * k + lane] = cur[k];
             __builtin_amdgcn_wave_barrier();
-            const bool more = tb + 8u < end;
-            if (more) cur = fetch(tb + 8u);
-            const uint32_t e = min(tb + 8u, end);
+            const bool more = tb + kT < end;
+            if (more) {
+#pragma unroll
+                for (uint32_t k = 0; k < RTX_PF_LDS; ++k) cur[k] = fetch(tb + kT, k);
+            }
+            const uint32_t e = min(tb + kT, end);
             for (; b < e; ++b) {
                 const float4 *q = tl + 8u * (b - tb);
                 float4 v[8];
@@ -337,7 +349,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
                 if (step(blk, b)) return b + 1;
             }
             if (!more) break;
-            tb += 8u;
+            tb += kT;
         }
     } else if constexpr (kPF) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
