@@ -38,8 +38,10 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 110 /* 1.1.0 */
+#define RTX_VERSION 120 /* 1.2.0 */
 /* ABI notes.
+ *  1.2.0: rtx_schedule.refill_chunk (a field before `reserved`: the struct
+ *         grew by 4 bytes).
  *  1.1.0: rtx_schedule_defaults / rtx_set_schedule / rtx_get_schedule (the
  *         chain-RNG schedule, formerly an undocumented environment variable
  *         of the library: the library now reads no environment);
@@ -183,7 +185,13 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     projected to need more than this many further ray segments hands it
  *     over at a sample boundary to a wave with nothing else to do (an idle
  *     render wave, or the tier-1 kernel), which traces it with all 64 lanes
- *     (0: never).
+ *     (0: never);
+ *   - refill_chunk: for a part of at least medium_share pixels per lane (a
+ *     whole frame), each wave takes its pixels from a private run of this
+ *     many consecutive slots of the cost-ordered queue, re-stocked when
+ *     empty, so its lanes hold pixels from few runs (coherent rays) rather
+ *     than one slot per refill from wherever the queue head is; the last
+ *     eighth of the queue is taken slot by slot.
  * Results never depend on the schedule (every pixel's operations are the
  * same whichever lanes trace it); only the time does. The defaults are the
  * measured best. A context starts with the defaults. */
@@ -214,6 +222,7 @@ typedef struct rtx_schedule {
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
+    uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
     uint32_t reserved;        /* must be 0 */
 } rtx_schedule;
 /* The library's defaults (no context, no GPU). */
@@ -222,7 +231,7 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
  * tail_coop_max and tail_coop_max_large in 1..64,
- * priorities in 0..3, reserved 0. */
+ * priorities in 0..3, refill_chunk in 0..4096, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 

@@ -262,6 +262,7 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
+    out->refill_chunk = t.chunk;
     return RTX_OK;
 }
 
@@ -296,6 +297,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         if (!(v >= 0.0f && v <= 0.5f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_* must be in [0, 0.5]");
     if (s->tier1_priority > 3 || s->tier2_priority > 3 || s->hot_priority > 3)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: priorities must be in 0..3");
+    if (s->refill_chunk > 4096) return fail(RTX_ERR_INVALID, "rtx_set_schedule: refill_chunk must be in 0..4096");
     if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
     rtx::KTune t;
     t.a1 = s->tier1_bar;
@@ -324,6 +326,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.prio_t1 = s->tier1_priority;
     t.prio_t2 = s->tier2_priority;
     t.prio_hot = s->hot_priority;
+    t.chunk = s->refill_chunk;
     c->tune = t;
     return RTX_OK;
 }
@@ -358,6 +361,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
+    out->refill_chunk = t.chunk;
     return RTX_OK;
 }
 

@@ -68,6 +68,7 @@ struct KParams {
     uint32_t coop_max;             // queue exhausted: a wave with <= this many pixels traces them in group coop
     uint32_t prio_t1, prio_t2, prio_hot;  // wave priorities (0..3) of tier-1, tier-2 and hot lane-mode waves
     uint32_t trace_ext;            // tier 1 runs in k_trace beside k_render (k_render skips it)
+    uint32_t chunk;                // refill: a wave's private run of this many queue slots (0 = one refill per need)
     // promotion (k_trace beside k_render): once its queue is empty, a lane-mode
     // wave hands a pixel whose projected remaining segments exceed prom_min
     // to k_trace at a sample boundary (rtx_kernels.hip, promote)
@@ -96,6 +97,7 @@ struct KTune {
     uint32_t coop_max;                      // KParams::coop_max (scenes with the coop's LDS copy)
     uint32_t coop_max_large;                // ... and without it (n > kCoopLds)
     uint32_t prio_t1, prio_t2, prio_hot;    // KParams::prio_*
+    uint32_t chunk;                         // KParams::chunk for a part of at least rho2 pixels per lane
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
 };

@@ -248,8 +248,8 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 // per-ray ku/kv of rtx_prefilter.h line_test_flat) or not (the 7-op test,
 // k0/k1 = nou/nov). Returns the block to resume at; `full` when it stopped
 // because some lane's list is full.
-#ifndef RTX_PF_LDS  // A/B build: large scenes stream through a per-wave LDS tile (below)
-#define RTX_PF_LDS 0
+#ifndef RTX_PF_LDS  // large scenes stream through a per-wave LDS tile of RTX_PF_LDS KiB (below; 0: SGPR double buffer)
+#define RTX_PF_LDS 1  // C5 1,880-1,907 -> 1,811-1,847 ms (profiles/R3w_*, R3x_*)
 #endif
 constexpr uint32_t kPfLdsBytes = (kRB / 64) * 64 * 16 * RTX_PF_LDS;  // RTX_PF_LDS KiB per wave
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
@@ -306,7 +306,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
         return false;
     };
     full = true;
-    if constexpr (kPF && RTX_PF_LDS) {
+    if (kPF && RTX_PF_LDS && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
         // A/B build: the scene streams through a per-wave
         // LDS tile of 8 * RTX_PF_LDS blocks (RTX_PF_LDS KiB: coalesced 16-byte
         // loads, one per lane per KiB, the next tile's loads in flight while
@@ -351,7 +351,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             if (!more) break;
             tb += kT;
         }
-    } else if constexpr (kPF) {
+    } else if (kPF) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
         f16v a_lo, a_hi, b_lo, b_hi;
         sload_blk(pre + 32 * b, a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
@@ -851,9 +851,7 @@ struct Lane {
     uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
     uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments)
     bool active;         // tracing a pixel
-#if RTX_CHUNK
-    uint32_t cb, ce;     // the wave's private run of queue slots (refill, A/B build)
-#endif
+    uint32_t cb, ce;     // the wave's private run of queue slots (refill; wave-uniform)
 };
 
 __device__ __forceinline__ void set_dir(Lane &L, f3 d) {
@@ -1213,9 +1211,6 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 // slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
 // per refill (ballot + lane rank). Returns true once the queue is
 // exhausted (wave-uniform).
-#ifndef RTX_CHUNK  // A/B build: private runs of queue slots per wave (refill)
-#define RTX_CHUNK 0
-#endif
 #ifndef RTX_REFILL_MIN  // A/B build: a wave with live lanes refills only once this many are idle
 #define RTX_REFILL_MIN 1  // (consecutive queue slots for more of its lanes: coherence vs idle lanes)
 #endif
@@ -1224,21 +1219,20 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
     if (idle == 0ull) return false;
     const uint32_t cnt = (uint32_t)__popcll(idle);
     if (RTX_REFILL_MIN > 1 && cnt < RTX_REFILL_MIN && cnt < 64u) return false;
-#if RTX_CHUNK
-    // A/B build: the wave's idle lanes take consecutive slots of a private
-    // run [cb, ce) of the queue, which is re-stocked RTX_CHUNK slots at a
-    // time, so that its lanes hold pixels from few runs of the cost order
-    // (coherent rays) instead of one slot per refill from wherever the queue
-    // head is. Off for the last eighth of the queue (no pixel waits in a
-    // busy wave's run while other waves are idle).
-    {
+    if (P.chunk > 1u) {
+        // The wave's idle lanes take consecutive slots of a private run
+        // [cb, ce) of the queue, re-stocked P.chunk slots at a time, so that
+        // its lanes hold pixels from few runs of the cost order (coherent
+        // rays) instead of one slot per refill from wherever the queue head
+        // is. Slot by slot for the last eighth of the queue (no pixel waits
+        // in a busy wave's run while other waves are idle).
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
         const uint32_t avail = L.ce - L.cb;
         uint32_t nb = 0, n = 0;
         if (cnt > avail) {
             n = cnt - avail;
-            if (L.cb < hi - (hi - lo) / 8u) n = max(n, (uint32_t)RTX_CHUNK);
+            if (L.cb < hi - (hi - lo) / 8u) n = max(n, P.chunk);
             if (lane == 0u) nb = atomicAdd(P.queue, n);
             nb = lo + (uint32_t)__shfl((int)nb, 0, 64);
         }
@@ -1252,15 +1246,12 @@ __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_
         }
         if (cnt > avail) {
             L.cb = nb + (cnt - avail);
-            L.ce = nb + n;
-            if (L.cb >= hi) return true;
-            L.ce = min(L.ce, hi);
-        } else {
-            L.cb += cnt;
+            L.ce = min(nb + n, hi);
+            return L.cb >= hi;
         }
+        L.cb += cnt;
         return false;
     }
-#endif
     const int leader = __ffsll((long long)idle) - 1;
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t base = 0;
@@ -1516,9 +1507,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     L.active = false;
     L.segs = 0;
     L.slot = ~0u;
-#if RTX_CHUNK
     L.cb = L.ce = 0u;
-#endif
     bool exhausted = !kPersist;
     if (!kPersist) {
         const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
@@ -1787,6 +1776,7 @@ KTune default_tune() {
     t.prio_t1 = 3;
     t.prio_t2 = 2;
     t.prio_hot = 3;
+    t.chunk = 16;  // C2 45.9 -> 44.5 ms, 12-16 best (profiles/R3w_*, R3x_*)
     t.trace_small = kTraceSmall;
     t.trace_low = kTraceLow;
     t.trace_medium = kTraceMedium;
@@ -2265,6 +2255,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     p.prio_t1 = tune.prio_t1;
     p.prio_t2 = tune.prio_t2;
     p.prio_hot = tune.prio_hot;
+    p.chunk = 0;
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t need = ceil_div(lanes, kRB);
@@ -2333,6 +2324,11 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
+    // private queue runs per wave for a large part only (a whole frame: R = 2,
+    // 4, 8 shares measured no better, profiles/R3x_parts.jsonl)
+    // and small scenes only (at 100k spheres a pixel takes ~100 ms in lane
+    // mode, and heavy pixels waited in busy waves' runs: C5 1.88 -> 2.05 s)
+    q.chunk = !pf && (double)lanes / ((double)blocks * kRB) >= tune.rho2 ? min(tune.chunk, 4096u) : 0u;
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     // tier 1 in k_trace on the auxiliary stream (small scenes): its waves

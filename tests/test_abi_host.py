@@ -49,7 +49,7 @@ def test_library_built_for_gfx950(rtx):
 
 def test_version_and_error_paths(rtx):
     lib = rtx.load_library()
-    assert lib.rtx_version() == 110
+    assert lib.rtx_version() == 120
     # null arguments are rejected without touching the GPU
     assert lib.rtx_upload_world(None, None) == -1
     assert b"null" in lib.rtx_last_error()
@@ -107,6 +107,7 @@ def test_schedule_defaults_and_validation(rtx):
     assert d.tier2_bar_medium == pytest.approx(1.2) and d.small_share == pytest.approx(1.2)
     assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
     assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 32 and d.tail_coop_max_large == 8
+    assert d.refill_chunk == 16
     assert d.tier2_bar == pytest.approx(1e30)
     assert (d.tier1_priority, d.tier2_priority, d.hot_priority) == (3, 2, 3)
     assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == (0.0, 0.0, 0.0, 0.0)

@@ -772,7 +772,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("refill_chunk", 5000),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})
@@ -838,6 +838,38 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
             got = buf.numpy()
             buf.free()
             assert_bits_equal(got, want_all[rows], f"{ctx_name} {sched} part {part} of {nparts}")
+            if nparts == 1:
+                assert st.segments == segs_all
+    ctx.set_schedule()
+
+
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+def test_refill_chunk_bit_exact(request, oracle, rtx, ctx_name):
+    """Private queue runs per wave (rtx_schedule.refill_chunk): with the share
+    classes moved down (medium_share 0.01) a 320x180 frame and its row shares
+    count as "large" parts, so every refill takes slots from the wave's run —
+    runs of 1 (off), 3, 16 and 500 slots (the last larger than the part, so
+    the last-eighth rule and the queue's end are crossed inside one run).
+    Bit for bit against the oracle, and the whole frame's segment count."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(11, depth=50, spp=12)
+    W, H, T = 320, 180, 5
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    want_all, segs_all = oracle.render_rows(world, frame, np.arange(H), nthreads=8)
+    for chunk in (0, 3, 16, 500):
+        ctx.set_schedule()
+        ctx.set_schedule(medium_share=0.01, low_share=0.005, small_share=0.001, refill_chunk=chunk)
+        for nparts, part in ((1, 0), (2, 1), (8, 5)):
+            rows = rtx.part_row_ids(H, T, part, nparts)
+            buf = ctx.alloc((len(rows), W, 4))
+            ctx.stats_reset()
+            ctx.render_rows(T, part, nparts, buf.ptr)
+            st = ctx.stats()
+            got = buf.numpy()
+            buf.free()
+            assert_bits_equal(got, want_all[rows], f"{ctx_name} chunk {chunk} part {part} of {nparts}")
             if nparts == 1:
                 assert st.segments == segs_all
     ctx.set_schedule()
