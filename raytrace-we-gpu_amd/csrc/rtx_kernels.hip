@@ -2248,6 +2248,9 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
     return hipGetLastError();
 }
 
+#ifndef RTX_PROM_LARGE  // A/B build: promotion for scenes without the coop's LDS copy too
+#define RTX_PROM_LARGE 0
+#endif
 hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
     const KTune &tune = sched.tune;  // validated by rtx_set_schedule
     KParams p = p_in;
@@ -2345,7 +2348,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // when it runs. Scenes with the coop's LDS copy only: at 100k spheres a
     // one-ray wave reads the scene from L2/HBM and is slower than lane mode
     // (C5 1.86 -> 2.39 s with promotion)
-    if (!pf && p.scene.n <= kCoopLds) {
+    if (RTX_PROM_LARGE || (!pf && p.scene.n <= kCoopLds)) {
         const double px_per_lane = (double)lanes / ((double)blocks * kRB);
         const double pm = px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
                           : px_per_lane < tune.rho2 ? tune.prom_medium : tune.prom_large;

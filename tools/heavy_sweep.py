@@ -26,6 +26,7 @@ ap.add_argument("--set", action="append", default=[])
 ap.add_argument("--grid", type=int, default=11, help="random_world grid half extent (159 + --max-spheres 100000: C5)")
 ap.add_argument("--max-spheres", type=int, default=0)
 ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--lib", default=None, help="librtx build to load (default: the product library)")
 a = ap.parse_args()
 
 from heavy_sweep_fields import schedule_of  # noqa: E402
@@ -34,7 +35,7 @@ from heavy_sweep_fields import schedule_of  # noqa: E402
 W, H, T = 1920, 1080, 5
 world = rtx.random_world(a.grid, capacity=a.max_spheres or None, depth=50, spp=a.spp)
 frame = rtx.camera_look_at(W, H, aspect=W / H)
-ctx = rtx.Context(0)
+ctx = rtx.Context(0, lib=rtx.load_library(a.lib) if a.lib else None)
 ctx.upload_world(world)
 ctx.set_frame(frame)
 buf = ctx.alloc((H, W, 4))
