@@ -40,8 +40,8 @@ extern "C" {
 
 #define RTX_VERSION 120 /* 1.2.0 */
 /* ABI notes.
- *  1.2.0: rtx_schedule.refill_chunk (a field before `reserved`: the struct
- *         grew by 4 bytes).
+ *  1.2.0: rtx_schedule.promote_big_scene (after promote_large) and
+ *         refill_chunk (before `reserved`): the struct grew by 8 bytes.
  *  1.1.0: rtx_schedule_defaults / rtx_set_schedule / rtx_get_schedule (the
  *         chain-RNG schedule, formerly an undocumented environment variable
  *         of the library: the library now reads no environment);
@@ -185,7 +185,9 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     projected to need more than this many further ray segments hands it
  *     over at a sample boundary to a wave with nothing else to do (an idle
  *     render wave, or the tier-1 kernel), which traces it with all 64 lanes
- *     (0: never);
+ *     (0: never); promote_big_scene replaces them for scenes above 640
+ *     spheres (no LDS copy: a segment is a long scan there, so a far
+ *     shorter remaining chain is worth handing to a whole wave);
  *   - refill_chunk: for a part of at least medium_share pixels per lane (a
  *     whole frame), each wave takes its pixels from a private run of this
  *     many consecutive slots of the cost-ordered queue, re-stocked when
@@ -197,8 +199,8 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  * measured best. A context starts with the defaults. */
 typedef struct rtx_schedule {
     float tier1_bar;          /* default 1.7 */
-    float tier1_bar_small;    /* default 4.0 */
-    float tier1_bar_low;      /* default 3.5 */
+    float tier1_bar_small;    /* default 2.5 */
+    float tier1_bar_low;      /* default 3.0 */
     float tier2_bar_small;    /* default 2.0 */
     float tier2_bar_medium;   /* default 1.2 */
     float tier2_bar;          /* default 1e30 (no tier 2 for a larger part) */
@@ -209,14 +211,15 @@ typedef struct rtx_schedule {
     float occupancy_small;    /* default 1.0; each occupancy in (0, 1] */
     float occupancy_low;      /* default 1.0 */
     float occupancy_normal;   /* default 1.0 */
-    float trace_small;        /* default 0; each trace_* in [0, 0.5] */
-    float trace_low;          /* default 0 */
+    float trace_small;        /* default 0.25; each trace_* in [0, 0.5] */
+    float trace_low;          /* default 0.2 */
     float trace_medium;       /* default 0 */
     float trace_large;        /* default 0 */
     float promote_small;      /* default 0; each promote_* in [0, 1e9] */
     float promote_low;        /* default 0 */
     float promote_medium;     /* default 500 */
     float promote_large;      /* default 400 */
+    float promote_big_scene;  /* default 60: every part of a scene above 640 spheres */
     uint32_t tail_coop_max;   /* default 32 */
     uint32_t tail_coop_max_large; /* default 8: the same for scenes above 640 spheres */
     uint32_t tier1_priority;  /* default 3 */

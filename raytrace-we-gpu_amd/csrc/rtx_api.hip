@@ -259,6 +259,7 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->promote_low = (float)t.prom_low;
     out->promote_medium = (float)t.prom_medium;
     out->promote_large = (float)t.prom_large;
+    out->promote_big_scene = (float)t.prom_big;
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
@@ -289,7 +290,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max must be in 1..64");
     if (s->tail_coop_max_large < 1 || s->tail_coop_max_large > 64)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: tail_coop_max_large must be in 1..64");
-    const float pr[] = {s->promote_small, s->promote_low, s->promote_medium, s->promote_large};
+    const float pr[] = {s->promote_small, s->promote_low, s->promote_medium, s->promote_large, s->promote_big_scene};
     for (float v : pr)
         if (!(v >= 0.0f && v <= 1e9f)) return fail(RTX_ERR_INVALID, "rtx_set_schedule: promote_* must be in [0, 1e9]");
     const float tr[] = {s->trace_small, s->trace_low, s->trace_medium, s->trace_large};
@@ -323,6 +324,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.prom_low = s->promote_low;
     t.prom_medium = s->promote_medium;
     t.prom_large = s->promote_large;
+    t.prom_big = s->promote_big_scene;
     t.prio_t1 = s->tier1_priority;
     t.prio_t2 = s->tier2_priority;
     t.prio_hot = s->hot_priority;
@@ -358,6 +360,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->promote_low = (float)t.prom_low;
     out->promote_medium = (float)t.prom_medium;
     out->promote_large = (float)t.prom_large;
+    out->promote_big_scene = (float)t.prom_big;
     out->tier1_priority = t.prio_t1;
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;

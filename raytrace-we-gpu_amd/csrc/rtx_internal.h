@@ -100,6 +100,7 @@ struct KTune {
     uint32_t chunk;                         // KParams::chunk for a part of at least rho2 pixels per lane
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
+    double prom_big;                                           // ... for scenes without the coop's LDS copy
 };
 KTune default_tune();
 
@@ -120,7 +121,10 @@ struct KSchedule {
     uint32_t epoch;     // launch counter: a promotion entry is ready when its last word equals it
 };
 constexpr uint32_t kCostBuckets = 256;
-constexpr uint32_t kCostSpp = 2;    // pre-pass samples per pixel (kept: the render resumes after them)
+#ifndef RTX_COST_SPP
+#define RTX_COST_SPP 2
+#endif
+constexpr uint32_t kCostSpp = RTX_COST_SPP;  // pre-pass samples per pixel (kept: the render resumes after them)
 constexpr uint32_t kCostSppLarge = 1;  // ... for scenes above kScanPfMin spheres (C5: 1,997 vs 2,018 ms)
 constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
 constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)

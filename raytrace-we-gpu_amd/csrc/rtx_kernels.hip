@@ -85,23 +85,27 @@ constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wa
 constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
 constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha * a lane's share of the summed keys
 constexpr double kHeavy1Alpha = 1.7;    // tier 1 iff key > alpha1 * share
-constexpr double kHeavy1AlphaSmall = 4.0;   // the same for a small frame share
+constexpr double kHeavy1AlphaSmall = 2.5;   // the same for a small frame share (4.0 until R4b: with k_trace)
 constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than this * resident lanes
-constexpr double kHeavy1AlphaLow = 3.5;     // tier-1 bar for a low share
+constexpr double kHeavy1AlphaLow = 3.0;     // tier-1 bar for a low share (3.5 until R4b)
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > this * share (2-way split: 37 -> 34 ms, r5a-b)
 constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (default: none)
 // k_trace waves (tier 1 outside k_render) as a fraction of the resident waves, by share class.
-// Measured (profiles/R3h_*): parts 8 / 4 / 2 are no faster with it (15.0-15.2 ms in-kernel vs
-// 16.2-16.6 with 20 %; 20.3 both; 30.7 vs 44 with 5 %: its few waves queue the many medium-share
-// tier-1 pixels), so it is off there; the whole frame is R3i.
-constexpr double kTraceSmall = 0.0, kTraceLow = 0.0, kTraceMedium = 0.0, kTraceLarge = 0.0;
+// With the tier-1 bars above: parts 8 15.75 -> 15.20 ms, parts 4 21.14 -> 20.57 ms (medians of 4,
+// profiles/R4b_sweep.jsonl; R3r/R3u swept the fractions and bars). Medium shares and the whole frame
+// are no faster with it (R3h: 30.7 vs 44 ms with 5 % at R = 2: its few waves queue the many
+// medium-share tier-1 pixels).
+constexpr double kTraceSmall = 0.25, kTraceLow = 0.2, kTraceMedium = 0.0, kTraceLarge = 0.0;
 // promotion thresholds (projected further segments; 0: off): a whole frame
 // 50.0 -> 46.5 ms at 300-500 (700: 48.5, 1000: 49-51); a 2-way split
 // 30.6-31.1 -> 29.6-30.0 ms at 250-500; 4- and 8-way splits 1-2 ms slower
 // at any threshold
 constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLarge = 400.0;
+// scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
+// pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
+constexpr double kPromBig = 60.0;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -1785,6 +1789,7 @@ KTune default_tune() {
     t.prom_low = kPromLow;
     t.prom_medium = kPromMedium;
     t.prom_large = kPromLarge;
+    t.prom_big = kPromBig;
     return t;
 }
 namespace {
@@ -2248,9 +2253,6 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
     return hipGetLastError();
 }
 
-#ifndef RTX_PROM_LARGE  // A/B build: promotion for scenes without the coop's LDS copy too
-#define RTX_PROM_LARGE 0
-#endif
 hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_t stream) {
     const KTune &tune = sched.tune;  // validated by rtx_set_schedule
     KParams p = p_in;
@@ -2345,12 +2347,14 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         trace_waves = (uint32_t)(frac * blocks * (kRB / 64) + 0.5);
     }
     // promotion: served by idle k_render waves, and by k_trace after tier 1
-    // when it runs. Scenes with the coop's LDS copy only: at 100k spheres a
-    // one-ray wave reads the scene from L2/HBM and is slower than lane mode
-    // (C5 1.86 -> 2.39 s with promotion)
-    if (RTX_PROM_LARGE || (!pf && p.scene.n <= kCoopLds)) {
+    // when it runs. Large scenes have their own threshold (prom_big): there a
+    // lane-mode segment is a 12.5k-block scan, so handing a far shorter
+    // remaining chain to a whole wave pays (an earlier "1.86 -> 2.39 s" at
+    // C5 was measured together with a 32-ray tail coop, R3u)
+    {
         const double px_per_lane = (double)lanes / ((double)blocks * kRB);
-        const double pm = px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
+        const double pm = p.scene.n > kCoopLds    ? tune.prom_big
+                          : px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
                           : px_per_lane < tune.rho2 ? tune.prom_medium : tune.prom_large;
         if (pm > 0.0 && sched.prom_q && sched.prom_cap > 0) {
             q.prom = sched.buckets + 2 * kCostBuckets + 4;  // zeroed with the buckets

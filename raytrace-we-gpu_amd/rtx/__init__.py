@@ -61,7 +61,7 @@ class rtx_schedule(C.Structure):
                 ("occupancy_small", C.c_float), ("occupancy_low", C.c_float), ("occupancy_normal", C.c_float),
                 ("trace_small", C.c_float), ("trace_low", C.c_float), ("trace_medium", C.c_float),
                 ("trace_large", C.c_float), ("promote_small", C.c_float), ("promote_low", C.c_float),
-                ("promote_medium", C.c_float), ("promote_large", C.c_float),
+                ("promote_medium", C.c_float), ("promote_large", C.c_float), ("promote_big_scene", C.c_float),
                 ("tail_coop_max", C.c_uint32), ("tail_coop_max_large", C.c_uint32), ("tier1_priority", C.c_uint32), ("tier2_priority", C.c_uint32),
                 ("hot_priority", C.c_uint32), ("refill_chunk", C.c_uint32), ("reserved", C.c_uint32)]
 

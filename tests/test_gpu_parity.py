@@ -772,7 +772,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("refill_chunk", 5000),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})

@@ -6,7 +6,7 @@ SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a
          "prio": "hot_fraction", "occs": "occupancy_small", "occl": "occupancy_low", "occn": "occupancy_normal",
          "coop": "tail_coop_max", "coopL": "tail_coop_max_large", "p1": "tier1_priority", "trs": "trace_small", "trl": "trace_low",
          "trm": "trace_medium", "trL": "trace_large", "prs": "promote_small", "prl": "promote_low",
-         "prm": "promote_medium", "prL": "promote_large", "p2": "tier2_priority", "ph": "hot_priority",
+         "prm": "promote_medium", "prL": "promote_large", "prB": "promote_big_scene", "p2": "tier2_priority", "ph": "hot_priority",
          "chunk": "refill_chunk"}
 
 
