@@ -94,7 +94,7 @@ constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > 
 constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (default: none)
 // k_trace waves (tier 1 outside k_render) as a fraction of the resident waves, by share class.
 // With the tier-1 bars above: parts 8 15.75 -> 15.20 ms, parts 4 21.14 -> 20.57 ms (medians of 4,
-// profiles/R4b_sweep.jsonl; R3r/R3u swept the fractions and bars). Medium shares and the whole frame
+// profiles/R4b_sweep_r4_r8_trace.jsonl; R3r/R3u swept the fractions and bars). Medium shares and the whole frame
 // are no faster with it (R3h: 30.7 vs 44 ms with 5 % at R = 2: its few waves queue the many
 // medium-share tier-1 pixels).
 constexpr double kTraceSmall = 0.25, kTraceLow = 0.2, kTraceMedium = 0.0, kTraceLarge = 0.0;
@@ -1846,6 +1846,9 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
 #ifndef RTX_PS_ITEM_MAJOR  // per-sample scratch layout: 1 = item-major (37.6 vs 38.5 ms, 8.8 vs 13.5 GB per C2 frame: R3u), 0 = sample-major
 #define RTX_PS_ITEM_MAJOR 1
 #endif
+#ifndef RTX_PS_TILE  // large scenes: the per-sample kernel's lane-mode scan streams through the LDS tile too
+#define RTX_PS_TILE 1
+#endif
 constexpr int kPsSlots = 4;
 constexpr uint32_t kPsStateBytes = (kRB / 64) * kPsSlots * 4 * sizeof(uint32_t);  // per block
 struct PsLane {
@@ -1919,6 +1922,9 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
     uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
+    // large scenes: the lane-mode scan's per-wave LDS tile (in the sphere copy's place)
+    const float *pf_tile =
+        kPF && RTX_PF_LDS && RTX_PS_TILE ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + kPsStateBytes) : nullptr;
     const SphGlobal sg = sph_global(P.scene);
     const uint32_t lane = threadIdx.x & 63u;
     if (lane < kPsSlots * 4) st[lane] = 0u;
@@ -1987,6 +1993,9 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
                 best = __uint_as_float(0x7f800000u);
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
+        } else if (kPF && pf_tile) {  // every lane of the wave fills the scan's LDS tile
+            hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a, L.inv_a,
+                                        kTMin, best, list, nullptr, 0, pf_tile, L.active);
         } else if (L.active) {
             hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list)
@@ -2211,7 +2220,7 @@ constexpr uint32_t kPsItems = RTX_PS_ITEMS;
 #endif
 constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
+    return (use_pf(s) ? list_bytes<true>() + (RTX_PS_TILE ? kPfLdsBytes : 0) : kListBytes) + kCoopBytes + kPsStateBytes +
            (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }

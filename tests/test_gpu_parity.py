@@ -844,6 +844,40 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
 
 
 @pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+def test_promotion_large_scene_bit_exact(request, oracle, rtx, ctx_name):
+    """Promotion in the large-scene (kPF) kernels, where the promoted pixel's
+    whole-wave trace reads the scene from `pre`/`cen` in HBM and the lane-mode
+    scan streams it through the per-wave LDS tile: 1,600 spheres (grid 20),
+    promote_big_scene 1 (nearly every pixel in flight once the queue is empty
+    is handed over; the queue overflows and lanes keep the rest) and the
+    default 60, whole frame and a 4-way share, bit for bit against the oracle,
+    and the frame's segment count."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(20, depth=50, spp=6)
+    assert world.count > 1024  # the kPF kernels
+    W, H, T = 192, 108, 3
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    ctx.upload_world(world)
+    ctx.set_frame(frame)
+    want_all, segs_all = oracle.render_rows(world, frame, np.arange(H), nthreads=8)
+    for thr in (1.0, 60.0):
+        ctx.set_schedule()
+        ctx.set_schedule(promote_big_scene=thr, medium_share=0.01, low_share=0.005, small_share=0.001)
+        for nparts, part in ((1, 0), (4, 1)):
+            rows = rtx.part_row_ids(H, T, part, nparts)
+            buf = ctx.alloc((len(rows), W, 4))
+            ctx.stats_reset()
+            ctx.render_rows(T, part, nparts, buf.ptr)
+            st = ctx.stats()
+            got = buf.numpy()
+            buf.free()
+            assert_bits_equal(got, want_all[rows], f"{ctx_name} promote {thr} part {part} of {nparts}")
+            if nparts == 1:
+                assert st.segments == segs_all
+    ctx.set_schedule()
+
+
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
 def test_refill_chunk_bit_exact(request, oracle, rtx, ctx_name):
     """Private queue runs per wave (rtx_schedule.refill_chunk): with the share
     classes moved down (medium_share 0.01) a 320x180 frame and its row shares
