@@ -513,7 +513,7 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
 // Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + 4], then the
 // per-pixel pre-pass state (float4, 16-byte aligned).
 static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 8 + 3) & ~(size_t)3; }
-constexpr uint32_t kPromCap = 65536;  // promotion queue entries (rtx::kPromWords words each)
+constexpr uint32_t kPromCap = 65536;  // promotion queue entries (8 words each)
 
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_render_rows: null ctx");
@@ -641,11 +641,10 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         c->d_sched = nullptr;
         c->sched_pixels = 0;
         // cost, perm, buckets; then 16-byte aligned per-pixel state
-        RTX_HIP(hipMalloc(&c->d_sched,
-                          (sched_state_off(npix) + 4 * npix + rtx::kPromWords * (size_t)kPromCap) * sizeof(uint32_t)));
+        RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix + 8 * (size_t)kPromCap) * sizeof(uint32_t)));
         // the promotion queue's epoch words start below every launch's epoch
         RTX_HIP(hipMemsetAsync(c->d_sched + sched_state_off(npix) + 4 * npix, 0,
-                               rtx::kPromWords * (size_t)kPromCap * sizeof(uint32_t), c->stream));
+                               8 * (size_t)kPromCap * sizeof(uint32_t), c->stream));
         c->sched_pixels = npix;
     }
     const size_t ps_need = rtx::ps_scratch_floats(p);

@@ -121,9 +121,6 @@ struct KSchedule {
     uint32_t epoch;     // launch counter: a promotion entry is ready when its last word equals it
 };
 constexpr uint32_t kCostBuckets = 256;
-// promotion queue entry: [0] gid [1] sample [2] seed [3..5] acc [6] 1 = mid-path
-// [7] epoch, then (mid-path) [8..10] o [11..13] d [14..16] col [17] bounce
-constexpr uint32_t kPromWords = 24;
 #ifndef RTX_COST_SPP
 #define RTX_COST_SPP 2
 #endif

@@ -106,12 +106,6 @@ constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLar
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
-#ifndef RTX_PROM_MID  // promotion inside a sample too (the entry carries the path), not only at sample boundaries
-#define RTX_PROM_MID 0
-#endif
-#ifndef RTX_PROM_ALLSERVE  // every idle render wave serves the promotion queue, not only the first of its block
-#define RTX_PROM_ALLSERVE 0
-#endif
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -1112,22 +1106,13 @@ __device__ __forceinline__ void agent_store_order() {
 // published with agent-scope atomics (the consumer may sit on another XCD,
 // whose L2 does not see these stores otherwise): the fields, a wait for their
 // completion, then the epoch word (agent_store_order).
-// mid: the lane is inside a sample (its path continues: o, d, col and bounce
-// travel with the entry); otherwise at a sample boundary.
-__device__ __forceinline__ bool promote(const KParams &P, const Lane &L, bool mid = false) {
-    const uint32_t done = max(L.sample - P.cost_spp, 1u);  // samples finished in this launch (0 mid-way through the first: 1)
+__device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
+    const uint32_t done = L.sample - P.cost_spp;  // samples traced in this launch (>= 1 here)
     const uint32_t segs = L.segs - L.seg0;
     if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
     const uint32_t slot = atomicAdd(&P.prom[0], 1u);
     if (slot >= P.prom_cap) return false;  // queue full: the lane keeps its pixel
-    uint32_t *e = P.prom_q + kPromWords * slot;
-    if (mid) {
-        const float v[10] = {L.o.x, L.o.y, L.o.z, L.d.x, L.d.y, L.d.z, L.col.x, L.col.y, L.col.z, 0.0f};
-#pragma unroll
-        for (int i = 0; i < 9; ++i) __hip_atomic_store(e + 8 + i, __float_as_uint(v[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(e + 17, L.bounce, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __hip_atomic_store(e + 6, mid ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *e = P.prom_q + 8u * slot;
     __hip_atomic_store(e + 0, L.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(e + 1, L.sample, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(e + 2, __float_as_uint(L.seed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1163,9 +1148,6 @@ __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L,
         } else {
             begin_sample(P, F, L.x, L.y, L);
         }
-    } else if (!kCost && RTX_PROM_MID && may_promote && promote(P, L, true)) {
-        L.active = false;  // mid-path: the entry carries the path's state
-        return true;
     }
     return false;
 }
@@ -1468,7 +1450,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         if (h < t && (threadIdx.x & 63u) == 0u) got = atomicCAS(&P.prom[1], h, h + 1u) == h ? h : ~0u;
         got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
         if (got != ~0u) {
-            const uint32_t *e = P.prom_q + kPromWords * got;
+            const uint32_t *e = P.prom_q + 8u * got;
             while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;  // 2 s at 100 MHz
@@ -1485,18 +1467,6 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
             W.seg0 = W.segs;
             W.slot = ~0u;
             W.active = true;
-            if (__hip_atomic_load(e + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {  // mid-path
-                float v[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i)
-                    v[i] = __uint_as_float(__hip_atomic_load(e + 8 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                W.o = mk3(v[0], v[1], v[2]);
-                set_dir(W, mk3(v[3], v[4], v[5]));  // a, inv_a: the same ops as when the path set d
-                W.col = mk3(v[6], v[7], v[8]);
-                W.bounce = __hip_atomic_load(e + 17, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                diag_pixel_start(P, W.gid, 3ull);
-                return true;
-            }
             begin_sample(P, F, W.x, W.y, W);
             diag_pixel_start(P, W.gid, 3ull);
             return true;
@@ -1573,7 +1543,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             uint32_t srv = 0;
             if ((threadIdx.x & 63u) == 0u) srv = atomicCAS(&s_server, 0u, threadIdx.x / 64u + 1u);
             srv = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)srv, 0, 64));
-            if (!RTX_PROM_ALLSERVE && srv != 0u && srv != threadIdx.x / 64u + 1u) break;  // another wave serves this block
+            if (srv != 0u && srv != threadIdx.x / 64u + 1u) break;  // another wave serves this block
             if (!take_promoted(P, F, npix, L)) break;
             L.active = (threadIdx.x & 63u) == 0u;  // one ray, traced by the whole wave (tier-1 coop)
             H.tier = 1;
