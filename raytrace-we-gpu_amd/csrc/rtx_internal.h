@@ -62,6 +62,7 @@ struct KParams {
     const uint32_t *perm;          // pixel queue order: slot -> local pixel (NULL = identity)
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
     uint32_t cost_spp;             // samples the pre-pass traced (the render resumes after them)
+    uint32_t cost_cap;             // pre-pass: a pixel still tracing after this many segments stops (0: none)
     float4 *state;                 // per pixel (acc, seed) after cost_spp samples: written by the
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
@@ -125,7 +126,10 @@ constexpr uint32_t kCostBuckets = 256;
 #define RTX_COST_SPP 2
 #endif
 constexpr uint32_t kCostSpp = RTX_COST_SPP;  // pre-pass samples per pixel (kept: the render resumes after them)
-constexpr uint32_t kCostSppLarge = 1;  // ... for scenes above kScanPfMin spheres (C5: 1,997 vs 2,018 ms)
+#ifndef RTX_COST_SPP_LARGE
+#define RTX_COST_SPP_LARGE 1
+#endif
+constexpr uint32_t kCostSppLarge = RTX_COST_SPP_LARGE;  // ... for scenes above kScanPfMin spheres (C5: 1,997 vs 2,018 ms)
 constexpr uint32_t kLptMinSpp = 8;  // below this the pre-pass costs more than it saves: exact grid
 constexpr uint32_t kBlock = 256;    // threads per block of the auxiliary kernels (4 waves)
 

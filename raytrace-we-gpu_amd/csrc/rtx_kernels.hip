@@ -106,6 +106,13 @@ constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLar
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
+#ifndef RTX_COST_CAP  // cost pre-pass: segments after which a pixel stops (the render traces it from sample 0)
+#define RTX_COST_CAP 0
+#endif
+#ifndef RTX_COST_CAP_LARGE
+#define RTX_COST_CAP_LARGE 0
+#endif
+constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -1107,7 +1114,10 @@ __device__ __forceinline__ void agent_store_order() {
 // whose L2 does not see these stores otherwise): the fields, a wait for their
 // completion, then the epoch word (agent_store_order).
 __device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
-    const uint32_t done = L.sample - P.cost_spp;  // samples traced in this launch (>= 1 here)
+    // samples traced in this launch (>= 1 here): after the pre-pass's cost_spp,
+    // or from 0 for a pixel the pre-pass stopped (cost_cap; then an upper
+    // bound of the rate once past cost_spp)
+    const uint32_t done = L.sample > P.cost_spp ? L.sample - P.cost_spp : max(L.sample, 1u);
     const uint32_t segs = L.segs - L.seg0;
     if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
     const uint32_t slot = atomicAdd(&P.prom[0], 1u);
@@ -1148,6 +1158,16 @@ __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L,
         } else {
             begin_sample(P, F, L.x, L.y, L);
         }
+    } else if (kCost && P.cost_cap != 0u && L.segs - L.seg0 >= P.cost_cap) {
+        // pre-pass: a pixel this long is heavy whatever its remaining
+        // samples cost; it stops here (its key: the cap) and the render
+        // traces it from sample 0 (state seed NaN). Its segments so far are
+        // not counted: the render redoes them with the same operations.
+        P.cost_out[L.gid] = P.cost_cap;
+        P.state[L.gid] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0x7fc00000u));
+        L.segs = L.seg0;
+        L.active = false;
+        diag_pixel_end(P, L.gid);
     }
     return false;
 }
@@ -1187,12 +1207,12 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
     L.gid = gid;
     lane_pixel(P, gid, L.x, L.y);
     L.seg0 = L.segs;
-    if (P.state && !P.cost_out) {  // after the pre-pass's cost_spp samples (identical state)
-        const float4 st = P.state[gid];
+    const float4 st = P.state && !P.cost_out ? P.state[gid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (P.state && !P.cost_out && !__builtin_isnan(st.w)) {  // after the pre-pass's cost_spp samples (identical state)
         L.acc = mk3(st.x, st.y, st.z);
         L.sample = P.cost_spp;
         L.seed = st.w;
-    } else {
+    } else {  // a fresh pixel, or one the pre-pass stopped (cost_cap)
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
         L.seed = pixel_seed(P, L.x, L.y, 0);
@@ -2296,6 +2316,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // large scenes: one sample — there a segment costs ~4 ms of wave time and
     // the pre-pass waits on its heaviest pixel's chain
     c.spp = min(p.spp, pf ? kCostSppLarge : kCostSpp);
+    c.cost_cap = pf ? kCostCapLarge : kCostCap;
     c.cost_out = sched.cost;
     c.state = sched.state;
     c.accum = nullptr;

@@ -68,6 +68,7 @@ for r in range(a.rounds):
         print(json.dumps({"variant": n, "round": r, "kernel_ms": round(times[n][-1], 3),
                           "wall_ms": round(wall * 1e3, 3),
                           "msamples_s": round(a.width * a.height * a.spp / (times[n][-1] * 1e-3) / 1e6, 1),
-                          "tests_per_s": st.sphere_tests / st.launches / (times[n][-1] * 1e-3)}), flush=True)
+                          "tests_per_s": st.sphere_tests / st.launches / (times[n][-1] * 1e-3),
+                          "segments_per_frame": st.segments // max(1, st.launches)}), flush=True)
 summary = {n: {"median_ms": round(float(np.median(t)), 3), "min_ms": round(float(min(t)), 3)} for n, t in times.items()}
 print(json.dumps({"summary": summary}))
