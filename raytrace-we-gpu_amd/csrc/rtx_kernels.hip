@@ -107,10 +107,10 @@ constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLar
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
 #ifndef RTX_COST_CAP  // cost pre-pass: segments after which a pixel stops (the render traces it from sample 0)
-#define RTX_COST_CAP 0
+#define RTX_COST_CAP 16  // C2 44.48 -> 43.72 ms (8: 48.05, 32: 43.99; profiles/R4g_ab_c2_prepass_cap.jsonl)
 #endif
-#ifndef RTX_COST_CAP_LARGE
-#define RTX_COST_CAP_LARGE 0
+#ifndef RTX_COST_CAP_LARGE  // the same above kScanPfMin spheres: off (C5 1,665 ms; 12: 1,666, 6: 1,952, 3: 2,347 —
+#define RTX_COST_CAP_LARGE 0  // at 1 spp the capped key under-rates heavy pixels, which then start late)
 #endif
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
