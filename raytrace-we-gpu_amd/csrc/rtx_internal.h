@@ -63,6 +63,7 @@ struct KParams {
     uint32_t *cost_out;            // cost pre-pass: per-pixel segment count instead of colour
     uint32_t cost_spp;             // samples the pre-pass traced (the render resumes after them)
     uint32_t cost_cap;             // pre-pass: a pixel still tracing after this many segments stops (0: none)
+    uint32_t cost_capped;          // ... and records this cost
     float4 *state;                 // per pixel (acc, seed) after cost_spp samples: written by the
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority

@@ -106,11 +106,15 @@ constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLar
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
-#ifndef RTX_COST_CAP  // cost pre-pass: segments after which a pixel stops (the render traces it from sample 0)
+// Cost pre-pass cap (whole-frame parts only: in a row-split share a capped,
+// under-rated key keeps heavy pixels out of the tiers — parts 2/4/8 30/21/15
+// -> 34/26/26 ms, profiles/R4h_parts.jsonl): a pixel still tracing after
+// this many segments stops, the render traces it from sample 0.
+#ifndef RTX_COST_CAP  // small scenes: the stopped pixel's cost is the cap
 #define RTX_COST_CAP 16  // C2 44.48 -> 43.72 ms (8: 48.05, 32: 43.99; profiles/R4g_ab_c2_prepass_cap.jsonl)
 #endif
-#ifndef RTX_COST_CAP_LARGE  // the same above kScanPfMin spheres: off (C5 1,665 ms; 12: 1,666, 6: 1,952, 3: 2,347 —
-#define RTX_COST_CAP_LARGE 0  // at 1 spp the capped key under-rates heavy pixels, which then start late)
+#ifndef RTX_COST_CAP_LARGE  // above kScanPfMin spheres (1-spp pre-pass): its cost saturates the key (top bucket)
+#define RTX_COST_CAP_LARGE 24  // C5 1,672 -> 1,623 ms (12: 1,659; the cap as the cost: 12 1,666, 6 1,952; R4g, R4h)
 #endif
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
@@ -1163,7 +1167,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L,
         // samples cost; it stops here (its key: the cap) and the render
         // traces it from sample 0 (state seed NaN). Its segments so far are
         // not counted: the render redoes them with the same operations.
-        P.cost_out[L.gid] = P.cost_cap;
+        P.cost_out[L.gid] = P.cost_capped;
         P.state[L.gid] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0x7fc00000u));
         L.segs = L.seg0;
         L.active = false;
@@ -2316,7 +2320,12 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // large scenes: one sample — there a segment costs ~4 ms of wave time and
     // the pre-pass waits on its heaviest pixel's chain
     c.spp = min(p.spp, pf ? kCostSppLarge : kCostSpp);
-    c.cost_cap = pf ? kCostCapLarge : kCostCap;
+    {
+        const uint32_t rb = resident_blocks(render_fn<true, false>(pf), lds);
+        const bool whole = (double)lanes >= tune.rho2 * (double)min(need, rb) * kRB;  // a large part (the tiers' class)
+        c.cost_cap = whole ? (pf ? kCostCapLarge : kCostCap) : 0u;
+        c.cost_capped = pf ? 0xffffu : c.cost_cap;
+    }
     c.cost_out = sched.cost;
     c.state = sched.state;
     c.accum = nullptr;
