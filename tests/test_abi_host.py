@@ -125,3 +125,31 @@ def test_library_reads_no_environment(rtx):
     schedule is an explicit C-ABI call): no getenv/secure_getenv import."""
     out = subprocess.run(["nm", "-D", "--undefined-only", rtx.LIB_PATH], capture_output=True, text=True).stdout
     assert "getenv" not in out, [l for l in out.splitlines() if "getenv" in l]
+
+
+def test_ctypes_mirror_matches_header_layout(rtx, tmp_path):
+    """The Python mirror's structs (rtx/__init__.py) have the sizes and field
+    offsets that include/rtx.h gives them under the C compiler, so a field
+    added to the header (ABI 1.2.0: promote_big_scene, refill_chunk) cannot
+    silently shift the mirror."""
+    import rtx as R
+    structs = {"rtx_world": R.rtx_world, "rtx_frame": R.rtx_frame, "rtx_schedule": R.rtx_schedule,
+               "rtx_stats": R.rtx_stats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rtx.h"', 'int main(void) {']
+    for name, cls in structs.items():
+        lines.append(f'  printf("{name} size %zu\\n", sizeof({name}));')
+        for field, _ in cls._fields_:
+            lines.append(f'  printf("{name} {field} %zu\\n", offsetof({name}, {field}));')
+    lines += ['  return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        *key, val = line.split()
+        got[tuple(key)] = int(val)
+    for name, cls in structs.items():
+        assert got[(name, "size")] == C.sizeof(cls), name
+        for field, _ in cls._fields_:
+            assert got[(name, field)] == getattr(cls, field).offset, (name, field)
