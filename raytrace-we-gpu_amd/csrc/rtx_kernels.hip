@@ -116,6 +116,9 @@ constexpr double kPromBig = 60.0;
 #ifndef RTX_COST_CAP_LARGE  // above kScanPfMin spheres (1-spp pre-pass): its cost saturates the key (top bucket)
 #define RTX_COST_CAP_LARGE 24  // C5 1,672 -> 1,623 ms (12: 1,659; the cap as the cost: 12 1,666, 6 1,952; R4g, R4h)
 #endif
+#ifndef RTX_PREPASS_CHUNK
+#define RTX_PREPASS_CHUNK 0
+#endif
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
@@ -2326,6 +2329,9 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         c.cost_cap = whole ? (pf ? kCostCapLarge : kCostCap) : 0u;
         c.cost_capped = pf ? 0xffffu : c.cost_cap;
     }
+    // A/B build: the persistent (large-scene) pre-pass refills its lanes from
+    // private runs of the index order too
+    c.chunk = pf ? (uint32_t)RTX_PREPASS_CHUNK : 0u;
     c.cost_out = sched.cost;
     c.state = sched.state;
     c.accum = nullptr;
