@@ -116,9 +116,6 @@ constexpr double kPromBig = 60.0;
 #ifndef RTX_COST_CAP_LARGE  // above kScanPfMin spheres (1-spp pre-pass): its cost saturates the key (top bucket)
 #define RTX_COST_CAP_LARGE 24  // C5 1,672 -> 1,623 ms (12: 1,659; the cap as the cost: 12 1,666, 6 1,952; R4g, R4h)
 #endif
-#ifndef RTX_PREPASS_CHUNK
-#define RTX_PREPASS_CHUNK 0
-#endif
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
@@ -1242,14 +1239,10 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 // slot of [lo, hi) (the queue counter counts from lo); ONE atomic per wave
 // per refill (ballot + lane rank). Returns true once the queue is
 // exhausted (wave-uniform).
-#ifndef RTX_REFILL_MIN  // A/B build: a wave with live lanes refills only once this many are idle
-#define RTX_REFILL_MIN 1  // (consecutive queue slots for more of its lanes: coherence vs idle lanes)
-#endif
 __device__ __forceinline__ bool refill(const KParams &P, const Frame &F, uint32_t lo, uint32_t hi, Lane &L) {
     const uint64_t idle = __ballot(!L.active);
     if (idle == 0ull) return false;
     const uint32_t cnt = (uint32_t)__popcll(idle);
-    if (RTX_REFILL_MIN > 1 && cnt < RTX_REFILL_MIN && cnt < 64u) return false;
     if (P.chunk > 1u) {
         // The wave's idle lanes take consecutive slots of a private run
         // [cb, ce) of the queue, re-stocked P.chunk slots at a time, so that
@@ -1873,9 +1866,6 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
 #ifndef RTX_PS_ITEM_MAJOR  // per-sample scratch layout: 1 = item-major (37.6 vs 38.5 ms, 8.8 vs 13.5 GB per C2 frame: R3u), 0 = sample-major
 #define RTX_PS_ITEM_MAJOR 1
 #endif
-#ifndef RTX_PS_TILE  // A/B build: the per-sample kernel's lane-mode scan of large scenes through the LDS tile
-#define RTX_PS_TILE 0   // (C5 per-sample 1,383 -> 1,666 ms with it: profiles/R4d_ab_c5_per_sample_tile.jsonl)
-#endif
 constexpr int kPsSlots = 4;
 constexpr uint32_t kPsStateBytes = (kRB / 64) * kPsSlots * 4 * sizeof(uint32_t);  // per block
 struct PsLane {
@@ -1949,9 +1939,6 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
     uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
-    // large scenes: the lane-mode scan's per-wave LDS tile (in the sphere copy's place)
-    const float *pf_tile =
-        kPF && RTX_PF_LDS && RTX_PS_TILE ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + kPsStateBytes) : nullptr;
     const SphGlobal sg = sph_global(P.scene);
     const uint32_t lane = threadIdx.x & 63u;
     if (lane < kPsSlots * 4) st[lane] = 0u;
@@ -2020,10 +2007,7 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
                 best = __uint_as_float(0x7f800000u);
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
-        } else if (kPF && pf_tile) {  // every lane of the wave fills the scan's LDS tile
-            hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a, L.inv_a,
-                                        kTMin, best, list, nullptr, 0, pf_tile, L.active);
-        } else if (L.active) {
+        } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
             hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list)
                           : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -2247,7 +2231,7 @@ constexpr uint32_t kPsItems = RTX_PS_ITEMS;
 #endif
 constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() + (RTX_PS_TILE ? kPfLdsBytes : 0) : kListBytes) + kCoopBytes + kPsStateBytes +
+    return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
            (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }
@@ -2329,9 +2313,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         c.cost_cap = whole ? (pf ? kCostCapLarge : kCostCap) : 0u;
         c.cost_capped = pf ? 0xffffu : c.cost_cap;
     }
-    // A/B build: the persistent (large-scene) pre-pass refills its lanes from
-    // private runs of the index order too
-    c.chunk = pf ? (uint32_t)RTX_PREPASS_CHUNK : 0u;
+    c.chunk = 0;  // (private runs for the large-scene pre-pass: no faster)
     c.cost_out = sched.cost;
     c.state = sched.state;
     c.accum = nullptr;
