@@ -38,8 +38,12 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 120 /* 1.2.0 */
+#define RTX_VERSION 130 /* 1.3.0 */
 /* ABI notes.
+ *  1.3.0: RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
+ *         rtx_stats_reset report a render launch that left pixels unwritten
+ *         (the promotion service's safety valve fired) instead of returning
+ *         the image as if it were complete.
  *  1.2.0: rtx_schedule.promote_big_scene (after promote_large) and
  *         refill_chunk (before `reserved`): the struct grew by 8 bytes.
  *  1.1.0: rtx_schedule_defaults / rtx_set_schedule / rtx_get_schedule (the
@@ -56,7 +60,10 @@ enum {
     RTX_ERR_INVALID = -1, /* bad argument (null pointer, size mismatch, ...) */
     RTX_ERR_HIP = -2,     /* a HIP runtime call failed */
     RTX_ERR_STATE = -3,   /* call out of order (no world / no frame yet) */
-    RTX_ERR_NOMEM = -4    /* host or device allocation failed */
+    RTX_ERR_NOMEM = -4,   /* host or device allocation failed */
+    RTX_ERR_INCOMPLETE = -5 /* a render launch since the last check left pixels
+                               unwritten (reported once, by the next rtx_sync,
+                               rtx_download, rtx_get_stats or rtx_stats_reset) */
 };
 
 /* Material type codes, as the reference stores them in WorldDef::matTypes
@@ -278,7 +285,7 @@ RTX_API int rtx_deinterleave_rows(rtx_ctx *ctx, const void *d_gathered,
                                   uint32_t tile_rows, uint32_t nparts,
                                   void *d_image);
 /* Wait for all work on the context stream (~ the implicit sync of Present,
- * DxCSApp.cpp:551). */
+ * DxCSApp.cpp:551); RTX_ERR_INCOMPLETE if a launch left pixels unwritten. */
 RTX_API int rtx_sync(rtx_ctx *ctx);
 /* Device pointer of the context framebuffer (width*height float4) or NULL. */
 RTX_API void *rtx_framebuffer(rtx_ctx *ctx);

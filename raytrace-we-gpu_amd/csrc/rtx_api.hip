@@ -49,6 +49,12 @@ struct EventPair {
 // has launches in flight, and a launch never blocks on an older one.
 constexpr size_t kEventRing = 64;  // initial ring size
 
+// Device counter words (unsigned long long): [0] ray segments, [2] pixel-queue
+// head (low half), [3] rtx_debug_pixel_cost's segments, [4] launch error bits
+// (rtx::kErr*, low half; read back and cleared by check_errors), [1], [5] spare.
+constexpr size_t kCounterWords = 6;
+constexpr size_t kErrWord = 4;
+
 }  // namespace
 
 #ifndef RTX_FLAT
@@ -108,6 +114,22 @@ namespace {
 int set_device(rtx_ctx *c) {
     RTX_HIP(hipSetDevice(c->device));
     return RTX_OK;
+}
+
+// After a stream synchronisation: the error bits the launches since the last
+// check set (KParams::errors), reported once and cleared. A set bit means a
+// launch left pixels unwritten (rtx_kernels.hip take_promoted).
+int check_errors(rtx_ctx *c, const char *what) {
+    unsigned long long bits = 0;
+    RTX_HIP(hipMemcpyAsync(&bits, c->d_counters + kErrWord, sizeof(bits), hipMemcpyDeviceToHost, c->stream));
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    if (bits == 0) return RTX_OK;
+    RTX_HIP(hipMemsetAsync(c->d_counters + kErrWord, 0, sizeof(bits), c->stream));
+    RTX_HIP(hipStreamSynchronize(c->stream));
+    std::string why;
+    if (bits & rtx::kErrPromTimeout) why += " promotion service saw no progress for 10 s and left;";
+    if (bits & rtx::kErrPromTorn) why += " a promotion entry was out of range;";
+    return fail(RTX_ERR_INCOMPLETE, std::string(what) + ": a render launch left pixels unwritten:" + why);
 }
 
 void free_world(rtx_ctx *c) {
@@ -186,8 +208,8 @@ int rtx_create(int hip_device, rtx_ctx **out) {
         return hip_fail(e, "hipStreamCreate");
     }
     c->stream = c->own_stream;
-    e = hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream);
+    e = hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
@@ -556,6 +578,7 @@ static rtx::KParams make_params(const rtx_ctx *c, uint32_t rows, uint32_t tile_r
     p.out = out;
     p.counters = c->d_counters;
     p.queue = reinterpret_cast<uint32_t *>(c->d_counters + 2);
+    p.errors = reinterpret_cast<uint32_t *>(c->d_counters + kErrWord);
     p.depth = c->depth;
     p.spp = c->spp;
     p.width = f.width;
@@ -707,7 +730,7 @@ int rtx_sync(rtx_ctx *c) {
     int rc = set_device(c);
     if (rc) return rc;
     RTX_HIP(hipStreamSynchronize(c->stream));
-    return RTX_OK;
+    return check_errors(c, "rtx_sync");
 }
 
 void *rtx_framebuffer(rtx_ctx *c) { return c ? c->d_fb : nullptr; }
@@ -721,14 +744,15 @@ int rtx_download(rtx_ctx *c, float *host, size_t bytes) {
     if (rc) return rc;
     RTX_HIP(hipMemcpyAsync(host, c->d_fb, bytes, hipMemcpyDeviceToHost, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
-    return RTX_OK;
+    return check_errors(c, "rtx_download");
 }
 
 int rtx_stats_reset(rtx_ctx *c) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_stats_reset: null ctx");
     int rc = set_device(c);
     if (rc) return rc;
-    RTX_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    rc = check_errors(c, "rtx_stats_reset");  // an unreported error of earlier launches
+    RTX_HIP(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
     c->ev_head = 0;
     c->ev_count = 0;
@@ -736,7 +760,7 @@ int rtx_stats_reset(rtx_ctx *c) {
     c->samples = 0;
     c->launches = 0;
     c->n_changed = false;
-    return RTX_OK;
+    return rc;
 }
 
 int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
@@ -745,6 +769,8 @@ int rtx_get_stats(rtx_ctx *c, rtx_stats *out) {
     int rc = set_device(c);
     if (rc) return rc;
     RTX_HIP(hipStreamSynchronize(c->stream));
+    rc = check_errors(c, "rtx_get_stats");
+    if (rc) return rc;
     unsigned long long h[4];
     RTX_HIP(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));

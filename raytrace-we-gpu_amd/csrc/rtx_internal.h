@@ -41,6 +41,10 @@ constexpr uint32_t kPad = 8;  // spheres per AoSoA block
 
 constexpr uint32_t kFrameLambertGuard = 1u;  // = RTX_FRAME_LAMBERT_GUARD
 
+// KParams::errors bits: a launch that sets one left pixels unwritten.
+constexpr uint32_t kErrPromTimeout = 1u;  // a promotion server saw no progress for kPromValveTicks and left
+constexpr uint32_t kErrPromTorn = 2u;     // a promotion entry held an out-of-range pixel or sample
+
 // Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
 struct KParams {
     KScene scene;
@@ -74,7 +78,8 @@ struct KParams {
     // promotion (k_trace beside k_render): once its queue is empty, a lane-mode
     // wave hands a pixel whose projected remaining segments exceed prom_min
     // to k_trace at a sample boundary (rtx_kernels.hip, promote)
-    uint32_t *prom;                // [0] entries claimed [1] entries taken [2] pixels written; NULL: off
+    uint32_t *prom;                // [0] entries claimed [1] entries taken [2] k_render-owned pixels written; NULL: off
+    uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)

@@ -34,6 +34,13 @@
 #include "rtx_internal.h"
 #include "rtx_prefilter.h"
 
+// The device code is written for gfx950 only: its wave64 DPP/permlane
+// exchanges, the s_waitcnt encoding of agent_store_order and the cross-XCD
+// promotion hand-off rely on that target's behaviour.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "rtx_kernels.hip targets gfx950 (MI355X) only"
+#endif
+
 namespace rtx {
 
 namespace {
@@ -858,13 +865,15 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
 }
 
 // Lane state: the pixel it is tracing and that pixel's current path.
+constexpr uint32_t kSeg0Restart = 0x80000000u;  // Lane::seg0 flag (a lane's segs stay far below 2^31)
 struct Lane {
     f3 o, d, col, acc;
     float a, inv_a, seed;
     uint32_t sample, bounce, segs;
     uint32_t x, y, gid;  // pixel (global image coords) and its output slot
     uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
-    uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments)
+    uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments);
+                         // kSeg0Restart: the render restarted it from sample 0 (cost_cap)
     bool active;         // tracing a pixel
     uint32_t cb, ce;     // the wave's private run of queue slots (refill; wave-uniform)
 };
@@ -1118,11 +1127,12 @@ __device__ __forceinline__ void agent_store_order() {
 // whose L2 does not see these stores otherwise): the fields, a wait for their
 // completion, then the epoch word (agent_store_order).
 __device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
-    // samples traced in this launch (>= 1 here): after the pre-pass's cost_spp,
-    // or from 0 for a pixel the pre-pass stopped (cost_cap; then an upper
-    // bound of the rate once past cost_spp)
-    const uint32_t done = L.sample > P.cost_spp ? L.sample - P.cost_spp : max(L.sample, 1u);
-    const uint32_t segs = L.segs - L.seg0;
+    // samples traced in this launch (>= 1 here): after the pre-pass's
+    // cost_spp, or from sample 0 for a pixel the pre-pass stopped (cost_cap;
+    // kSeg0Restart in seg0)
+    const bool restarted = (L.seg0 & kSeg0Restart) != 0u;
+    const uint32_t done = max(restarted ? L.sample : L.sample - min(L.sample, P.cost_spp), 1u);
+    const uint32_t segs = L.segs - (L.seg0 & ~kSeg0Restart);
     if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
     const uint32_t slot = atomicAdd(&P.prom[0], 1u);
     if (slot >= P.prom_cap) return false;  // queue full: the lane keeps its pixel
@@ -1220,6 +1230,7 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
         L.seed = pixel_seed(P, L.x, L.y, 0);
+        if (P.state && !P.cost_out) L.seg0 |= kSeg0Restart;  // promote() counts its samples from 0
     }
     L.active = true;
     begin_sample(P, F, L.x, L.y, L);
@@ -1449,23 +1460,44 @@ __device__ __forceinline__ void trace_pixel_uniform(const KParams &P, const Fram
 
 // Promotion queue service: wait for an entry and load it into W (every lane
 // the same state, at the entry's sample boundary), or return false once every
-// pixel of the launch is written (prom[2], counted by the writers: k_render
-// waves when they go idle, k_trace per pixel) — promoted pixels are counted
-// by whoever finishes them, so the count reaches npix only when the queue
-// holds nothing more. The tail is read after the count: a pixel is promoted
-// (slot claimed, entry stored) before its old wave can go idle and flush.
-// All relaxed (agent_store_order). Polls sleep ~8k clocks at priority 0;
-// safety valve: a wave that finds nothing for 2 s leaves (a bug would then
-// show as unwritten pixels, never as a hung GPU).
-__device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, uint32_t npix, Lane &W) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+// pixel k_render owns is written. prom[2] counts them (k_render waves when
+// they go idle; whoever finishes a promoted pixel), `target` is their number
+// (npix, less tier 1 when k_trace runs it): k_trace's own pixels are not in
+// it, so k_render's exit never waits for k_trace, which HIP does not promise
+// to run at the same time. Promoted pixels are counted by whoever finishes
+// them, so the count reaches `target` only when the queue holds nothing
+// more. The tail is read after the count: a pixel is promoted (slot claimed,
+// entry stored) before its old wave can go idle and flush. `helper` (k_trace):
+// serve only while k_render runs — prom[3] counts its started workgroups; a
+// k_trace that sees none leaves (k_render then serves its own promotions),
+// one that sees some waits on a kernel that is already running. All relaxed
+// (agent_store_order). Polls sleep ~8k clocks at priority 0. Safety valve: a
+// server that sees no pixel written for kPromValveTicks leaves and flags the
+// launch (KParams::errors: rtx_sync / rtx_get_stats report it), so a bug shows
+// as an error, never as a hung GPU or a silently unwritten pixel.
+constexpr unsigned long long kPromValveTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+__device__ __forceinline__ void flag_error(const KParams &P, uint32_t bit) {
+    if (P.errors && (threadIdx.x & 63u) == 0u) atomicOr(P.errors, bit);
+}
+__device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, uint32_t npix, uint32_t target,
+                                              bool helper, Lane &W) {
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t seen = ~0u;
     __builtin_amdgcn_s_setprio(0);
+    auto ld = [](const uint32_t *p) {
+        return (uint32_t)__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
     for (;;) {
-        const uint32_t done = __hip_atomic_load(&P.prom[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done >= npix) return false;
+        const uint32_t done = ld(&P.prom[2]);
+        if (done >= target) return false;
+        if (helper && ld(&P.prom[3]) == 0u) return false;  // k_render has not started: it serves itself
+        if (done != seen) {  // progress: the valve restarts
+            seen = done;
+            t0 = __builtin_amdgcn_s_memrealtime();
+        }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        const uint32_t t = min(__hip_atomic_load(&P.prom[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.prom_cap);
-        const uint32_t h = __hip_atomic_load(&P.prom[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t = min(ld(&P.prom[0]), P.prom_cap);
+        const uint32_t h = ld(&P.prom[1]);
         uint32_t got = ~0u;
         if (h < t && (threadIdx.x & 63u) == 0u) got = atomicCAS(&P.prom[1], h, h + 1u) == h ? h : ~0u;
         got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
@@ -1473,7 +1505,10 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
             const uint32_t *e = P.prom_q + 8u * got;
             while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;  // 2 s at 100 MHz
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
+                    flag_error(P, kErrPromTimeout);
+                    return false;
+                }
             }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the fields are read after the epoch matched
             W.gid = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1482,7 +1517,10 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
             W.acc = mk3(__uint_as_float(__hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                         __uint_as_float(__hip_atomic_load(e + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                         __uint_as_float(__hip_atomic_load(e + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-            if (W.gid >= npix || W.sample >= P.spp) return false;  // never: a torn entry ends the wave, not the GPU
+            if (W.gid >= npix || W.sample >= P.spp) {  // never: a torn entry ends the wave, not the GPU
+                flag_error(P, kErrPromTorn);
+                return false;
+            }
             lane_pixel(P, W.gid, W.x, W.y);
             W.seg0 = W.segs;
             W.slot = ~0u;
@@ -1492,7 +1530,10 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
             return true;
         }
         if (h >= t) __builtin_amdgcn_s_sleep(127);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
+            flag_error(P, kErrPromTimeout);
+            return false;
+        }
     }
 }
 
@@ -1521,7 +1562,10 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
     if (kPF && threadIdx.x == 0) *pack = 0u;
-    if (prom_on && threadIdx.x == 0) s_server = 0u;
+    if (prom_on && threadIdx.x == 0) {
+        s_server = 0u;
+        __hip_atomic_fetch_add(&P.prom[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_render runs
+    }
     if (coop_lds || kPF || prom_on) __syncthreads();
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
@@ -1545,7 +1589,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
-    uint32_t written = 0;  // pixels this wave wrote since it last reported (promotion's exit count)
+    // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
+    const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
+    uint32_t written = 0;  // pixels this wave wrote since it last reported
     Diag D;
     D.begin();
     for (;;) {
@@ -1564,7 +1610,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             if ((threadIdx.x & 63u) == 0u) srv = atomicCAS(&s_server, 0u, threadIdx.x / 64u + 1u);
             srv = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)srv, 0, 64));
             if (srv != 0u && srv != threadIdx.x / 64u + 1u) break;  // another wave serves this block
-            if (!take_promoted(P, F, npix, L)) break;
+            if (!take_promoted(P, F, npix, owned, false, L)) break;
             L.active = (threadIdx.x & 63u) == 0u;  // one ray, traced by the whole wave (tier-1 coop)
             H.tier = 1;
             continue;
@@ -1670,15 +1716,15 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
         if (threadIdx.x == 0) {
             write_pixel<false>(P, W);
             diag_pixel_end(P, W.gid);
-            if (P.prom) __hip_atomic_fetch_add(&P.prom[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         segs += W.segs;
     }
-    // then the promotion queue, until every pixel of the launch is written
+    // then, while k_render runs, help serve the promotion queue until every
+    // pixel k_render owns (all but tier 1) is written
     if (P.prom) {
         Lane W;
         W.segs = 0;
-        while (take_promoted(P, F, npix, W)) {
+        while (take_promoted(P, F, npix, npix - k1, true, W)) {
             const uint32_t s0 = W.segs;
             set_prio(P.prio_t1);
             trace_pixel_uniform(P, F, sl, W, nullptr, nullptr);

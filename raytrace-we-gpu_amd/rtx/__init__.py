@@ -26,6 +26,8 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RTX_LIB", os.path.join(_PKG_DIR, "lib", "librtx.so"))
 
 RTX_OK = 0
+RTX_ERR_INCOMPLETE = -5  # a render launch left pixels unwritten (ABI 1.3)
+SCHEDULE_ABI = 120  # the rtx_schedule layout this module passes (ABI 1.2.0)
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
@@ -257,10 +259,20 @@ def part_row_ids(height: int, tile_rows: int, part: int, nparts: int) -> np.ndar
     return y[(y // tile_rows) % nparts == part].astype(np.uint32)
 
 
+def _require_schedule_abi(lib: C.CDLL):
+    """rtx_schedule grew in 1.2.0 (promote_big_scene, refill_chunk): an
+    older library would read this module's struct at the wrong offsets."""
+    v = int(lib.rtx_version())
+    if v < SCHEDULE_ABI or not hasattr(lib, "rtx_set_schedule"):
+        raise RtxError(f"library ABI {v} predates the rtx_schedule layout {SCHEDULE_ABI} this binding passes")
+
+
 def schedule_defaults() -> rtx_schedule:
     """The library's default schedule (no GPU)."""
+    lib = load_library()
+    _require_schedule_abi(lib)
     sch = rtx_schedule()
-    _check(load_library().rtx_schedule_defaults(C.byref(sch)), "rtx_schedule_defaults")
+    _check(lib.rtx_schedule_defaults(C.byref(sch)), "rtx_schedule_defaults")
     return sch
 
 
@@ -370,6 +382,7 @@ class Context:
     def set_schedule(self, schedule: Optional[rtx_schedule] = None, **fields):
         """Install a schedule (rtx_set_schedule): `schedule`, or the current
         one with `fields` replaced; no arguments = the defaults."""
+        _require_schedule_abi(self._lib)
         if schedule is None and not fields:
             _check(self._lib.rtx_set_schedule(self._h, None), "rtx_set_schedule", self._lib)
             return
@@ -381,6 +394,7 @@ class Context:
         _check(self._lib.rtx_set_schedule(self._h, C.byref(sch)), "rtx_set_schedule", self._lib)
 
     def get_schedule(self) -> rtx_schedule:
+        _require_schedule_abi(self._lib)
         sch = rtx_schedule()
         _check(self._lib.rtx_get_schedule(self._h, C.byref(sch)), "rtx_get_schedule", self._lib)
         return sch

@@ -49,7 +49,7 @@ def test_library_built_for_gfx950(rtx):
 
 def test_version_and_error_paths(rtx):
     lib = rtx.load_library()
-    assert lib.rtx_version() == 120
+    assert lib.rtx_version() == 130
     # null arguments are rejected without touching the GPU
     assert lib.rtx_upload_world(None, None) == -1
     assert b"null" in lib.rtx_last_error()
@@ -153,3 +153,19 @@ def test_ctypes_mirror_matches_header_layout(rtx, tmp_path):
         assert got[(name, "size")] == C.sizeof(cls), name
         for field, _ in cls._fields_:
             assert got[(name, field)] == getattr(cls, field).offset, (name, field)
+
+
+def test_schedule_calls_refuse_an_older_abi(rtx):
+    """rtx_schedule grew in ABI 1.2.0: the binding refuses to pass its layout to
+    a library that reports an older version (it would read the fields after
+    promote_large at the wrong offsets) instead of installing a wrong schedule."""
+    class OldLib:
+        def rtx_version(self):
+            return 110
+
+        def rtx_set_schedule(self, *a):
+            raise AssertionError("must not be called")
+
+    with pytest.raises(rtx.RtxError, match="predates"):
+        rtx._require_schedule_abi(OldLib())
+    rtx._require_schedule_abi(rtx.load_library())  # the in-tree library passes
