@@ -12,11 +12,20 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -ff
 LIB       := $(LIBDIR)/librtx.so
 CLI       := $(BINDIR)/rtx_cli
 HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)/rtx_prefilter.h
+# Build provenance (rtx_build_info): the library records the hash of the
+# sources it was built from; bench.py compares it with the tree's
+# (tools/src_sha.py computes the same hash).
+LIBSRCS   := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/*.cpp)) include/rtx.h
+SRC_SHA   := $(shell python3 tools/src_sha.py)
 
 all: $(LIB) $(CLI) oracle $(LIBDIR)/variants/librtx_stress.so
 
 $(LIBDIR)/%.o: $(SRC)/%.hip $(HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# rtx_api.o carries the source hash: rebuilt whenever any library source changes
+$(LIBDIR)/rtx_api.o: $(SRC)/rtx_api.hip $(LIBSRCS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DRTX_SRC_SHA='"$(SRC_SHA)"' -c $< -o $@
 
 $(LIBDIR)/rtx_host.o: $(SRC)/rtx_host.cpp include/rtx.h | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -65,7 +74,7 @@ variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
 $(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS)
 	mkdir -p $(VDIR)/$*
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$*/k.o
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -DRTX_SRC_SHA='"$(SRC_SHA)"' -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(VDIR)/$*/k.o $(VDIR)/$*/a.o $(VDIR)/$*/h.o
 

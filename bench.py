@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "raytrace-we-gpu_amd"))
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-FLOP_PER_TEST = 20        # algorithmic FLOP per ray-sphere test
+FLOP_PER_TEST = 20        # the reference algorithm's FLOP per ray-sphere test (effective rate)
 
 
 def parse():
@@ -80,7 +80,7 @@ def probe(args):
         ctx.sync()
 
 
-def _pmc_pass(args, counters, tag):
+def _pmc_pass(args, counters, tag, rng=None):
     """One rocprofv3 --pmc pass over the --probe child (one frame through
     the C-ABI). Returns {counter: summed value over the k_render dispatches},
     or raises RuntimeError."""
@@ -89,7 +89,7 @@ def _pmc_pass(args, counters, tag):
         raise RuntimeError("rocprofv3 not found")
     base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
             "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
-            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", args.rng]
+            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", rng or args.rng]
     out = tempfile.mkdtemp(prefix=f"rtx_pmc_{tag}_")
     cmd = [exe, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
     try:
@@ -130,13 +130,16 @@ SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CY
                "GRBM_GUI_ACTIVE"]
 
 
-def pmc_valu(args, n_cu, launch_ms):
-    """Executed-work view of the render launch (its own --pmc pass): how busy
-    the VALU issue was and how many lanes each VALU instruction had.
-    SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8
-    XCDs (MI355X_MICROARCH.md, cycle constants)."""
+VALU_ISSUE_MAX = 0.25  # wave64 VALU instructions per cycle per SIMD (16 lanes: 4 cycles each)
+
+
+def pmc_valu(args, n_cu, launch_ms, rng=None):
+    """Executed-work view of the render launch (its own --pmc pass): the FP32
+    FLOPs the VALU ran, how busy the VALU issue was and how many lanes each
+    VALU instruction had. SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE
+    is summed over the 8 XCDs (MI355X_MICROARCH.md, cycle constants)."""
     try:
-        v = _pmc_pass(args, SQ_COUNTERS, "sq")
+        v = _pmc_pass(args, SQ_COUNTERS, "sq", rng)
     except RuntimeError as e:
         return {"skipped": str(e)}
     cycles = v["GRBM_GUI_ACTIVE"] / 8.0
@@ -146,18 +149,49 @@ def pmc_valu(args, n_cu, launch_ms):
     lane_util = v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"])
     flops = 64.0 * (v["SQ_INSTS_VALU_FLOPS_FP32"] + v["SQ_INSTS_VALU_FLOPS_FP32_TRANS"])
     tflops = flops / (launch_ms * 1e-3) / 1e12
+    ipc = v["SQ_INSTS_VALU"] / (simds * cycles)
     return {"executed_tflops": round(tflops, 3), "executed_frac": round(tflops / FP32_PEAK_TFLOPS, 4),
             "executed_tflops_active_lanes": round(tflops * lane_util, 3),
             "executed_flop_per_launch": flops,
+            "issue_frac": round(ipc / VALU_ISSUE_MAX, 4),
             "valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
-            "valu_lane_util": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
-            "valu_insts_per_simd_cycle": round(v["SQ_INSTS_VALU"] / (simds * cycles), 4),
+            "valu_lane_util": round(lane_util, 4),
+            "valu_insts_per_simd_cycle": round(ipc, 4),
+            "flop_per_valu_inst": round(flops / 64.0 / max(1.0, v["SQ_INSTS_VALU"]), 3),
             "formula": "executed = 64 * (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS) / launch time (the FP32 FLOPs "
                        "the VALU ran, prefilter, exact tests and shading included; _active_lanes scales by "
-                       "valu_lane_util); "
+                       "valu_lane_util); issue_frac = SQ_INSTS_VALU / (4*CUs * GRBM_GUI_ACTIVE/8 * 0.25) "
+                       "(wave64 VALU instructions issued per SIMD-cycle over their limit); "
                        "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8) (rocprof VALUBusy); "
                        "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)",
             "counters": v, "cus": n_cu}
+
+
+def roofline_of(executed, launch_ms, tests_per_launch):
+    """The compute roofline of one launch. `frac` is the EXECUTED FP32 FLOP
+    rate over the FP32 peak (PMC counters over the live launch time: <= 1 by
+    construction); `issue_frac` is the VALU-issue fraction, the roof that
+    binds this kernel (its instructions are mostly not full-rate FMAs, so it
+    saturates issue at under half the FLOP peak). The reference-algorithm
+    rate — 20 FLOP for every ray-sphere test of every segment — is reported
+    as `effective_tflops`: an effective-work rate, not a roofline fraction
+    (the prefilter executes 5-7 FLOP per test plus exact tests of the few
+    flagged spheres, so it can exceed what the ALUs run)."""
+    eff = FLOP_PER_TEST * tests_per_launch / (launch_ms * 1e-3) / 1e12
+    r = {"bound": "fp32-valu", "binding": "VALU issue (issue_frac)",
+         "roof": "fp32 vector ALU, 157.3 TF; VALU issue 0.25 wave-instructions/cycle/SIMD (the kernel issues no MFMA)",
+         "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None,
+         "frac_kind": "executed FP32 FLOP/s / FP32 peak",
+         "issue_frac": None}
+    if executed and "executed_tflops" in executed:
+        r.update(achieved=executed["executed_tflops"], frac=executed["executed_frac"],
+                 issue_frac=executed["issue_frac"])
+    else:
+        r["frac_kind"] += " (needs the N=1 PMC passes: not run here)"
+    r.update(effective_tflops=round(eff, 3),
+             effective_note="20 FLOP x (segments x spheres) per launch / launch time: the reference algorithm's "
+                            "work rate, not a fraction of any roof")
+    return r
 
 
 def cpu_baseline(args, world, frame, gpu_image, budget_s):
@@ -229,6 +263,41 @@ def host_cpu():
     except OSError:
         pass
     return {"nproc": os.cpu_count(), "model": model}
+
+
+def launch_desc(n_spheres, spp, nparts, rng):
+    """What one rtx_render_rows launch runs for this configuration
+    (rtx_kernels.hip launch_render / launch_ps)."""
+    if spp < 8 and rng == "chain":
+        return "rtx_render_rows launch = k_render<false> (exact grid, one lane per pixel)"
+    large = ((n_spheres + 7) // 8) * 8 > 1024  # kScanPfMin: the kPF kernels
+    scan = ("lane-mode scan streamed through a per-wave LDS tile, candidate lists of 24"
+            if large else "scalar-loaded scan, resolve from the block's LDS copy of the scene")
+    if rng == "per-sample":
+        return f"k_render_ps (one lane per pixel-sample, in-order fold per pixel; {scan.split(',')[0]})"
+    whole = nparts == 1
+    if large:
+        pre = ("k_render<true,true,kPF> 1-spp cost pre-pass on persistent lanes (sample 0, resumed from"
+               + ("; a pixel past 24 segments stops with a saturated key and restarts in the render)" if whole
+                  else ")"))
+    else:
+        pre = ("k_render<false,true> 2-spp exact-grid cost pre-pass (samples 0-1, resumed from"
+               + ("; a pixel past 16 segments stops and restarts in the render)" if whole else ")"))
+    return (f"rtx_render_rows launch = {pre} + k_cost_hist + k_heavy_split + k_cost_scatter + "
+            f"k_render<true> (cost-ordered persistent lanes, {scan}, heavy-pixel coop tiers, promotion)"
+            + (" [+ k_trace on the aux stream for a small or low share]" if not large and not whole else ""))
+
+
+def build_provenance(rtx):
+    """The loaded library and whether it was built from this tree's sources
+    (rtx_build_info's hash vs tools/src_sha.py over the same files)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from src_sha import src_sha16
+    info = rtx.build_info()
+    tree = src_sha16(ROOT)
+    return {"lib": os.path.relpath(rtx.LIB_PATH, ROOT), "lib_src_sha16": info.get("src_sha16"),
+            "tree_src_sha16": tree, "built_from_this_tree": info.get("src_sha16") == tree,
+            "arch": info.get("arch")}
 
 
 def main():
@@ -305,14 +374,13 @@ def main():
         value = samples / elapsed / 1e6
         launch_ms = st.kernel_ms / max(1, st.launches)
         tests_per_launch = st.sphere_tests / max(1, st.launches)
-        flops = FLOP_PER_TEST * tests_per_launch
-        achieved = flops / (launch_ms * 1e-3) / 1e12
         rows0 = rtx.part_rows(H, T, 0, R) if R > 1 else H
         alg_bytes = rows0 * W * 16 + world.count * 32  # framebuffer + scene
-        traffic, pmc_note, executed = (None, "skipped", None)
+        n_cu = torch.cuda.get_device_properties(local_rank).multi_processor_count
+        traffic, pmc_note, executed = (None, "skipped (PMC passes run at N=1 with --pmc auto)", None)
         if args.pmc == "auto" and R == 1:
             traffic, pmc_note = pmc_traffic(args)
-            executed = pmc_valu(args, torch.cuda.get_device_properties(local_rank).multi_processor_count, launch_ms)
+            executed = pmc_valu(args, n_cu, launch_ms)
         host_img = image.cpu().numpy() if R == 1 else None
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
@@ -336,16 +404,23 @@ def main():
             t_ps = (time.perf_counter() - t_ps) / n_ps
             st_ps = ctx.stats()
             ps_ms = st_ps.kernel_ms / max(1, st_ps.launches)
-            ps_flops = FLOP_PER_TEST * st_ps.sphere_tests / max(1, st_ps.launches)
+            ps_exec = pmc_valu(args, n_cu, ps_ms, rng="per-sample") if args.pmc == "auto" else None
             per_sample = {"value": round(W * H * args.spp / t_ps / 1e6, 3), "unit": "Msamples/s",
                           "ms_per_step": round(t_ps * 1e3, 3), "steps": n_ps, "kernel_ms": round(ps_ms, 4),
-                          "frac": round(ps_flops / (ps_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
-                          "kernel": "k_render_ps (one lane per pixel-sample, in-order fold per pixel)"}
+                          "roofline": roofline_of(ps_exec, ps_ms, st_ps.sphere_tests / max(1, st_ps.launches)),
+                          "executed": ps_exec,
+                          "kernel": launch_desc(world.count, args.spp, R, "per-sample")}
             if args.cpu_seconds > 0:
                 rows_ps = [int(r) for r in np.linspace(5, H - 6, 16)]  # 16 rows spread over the image
                 per_sample["parity"] = per_sample_parity(world, frame, image.cpu().numpy(), rows_ps)
             frame.rng_mode = 0
             ctx.set_frame(frame)
+        roof = roofline_of(executed, launch_ms, tests_per_launch)
+        roof.update(traffic=None if traffic is None else round(traffic),
+                    kernel=launch_desc(world.count, args.spp, R, args.rng), kernel_ms=round(launch_ms, 4),
+                    sphere_tests_per_launch=tests_per_launch,
+                    segments_per_sample=round(st.segments / max(1, st.samples), 4),
+                    pmc=pmc_note, executed=executed)
         line = {
             "metric": "Msamples/sec (pixels x spp) at 1920x1080 spp=100 depth=50",
             "value": round(value, 3),
@@ -364,19 +439,7 @@ def main():
                        "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                        "spheres": world.count, "rng": args.rng, "tile_rows": T,
                        "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if R > 1 else "")},
-            "roofline": {"bound": "fp32-valu", "roof": "fp32 vector ALU, 157.3 TF (the kernel issues no MFMA)",
-                         "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                         "traffic": None if traffic is None else round(traffic),
-                         "kernel": ("rtx_render_rows launch = k_render<false,true> 2-spp cost pre-pass (samples 0-1, "
-                                    "resumed from) + k_cost_hist + k_heavy_split + k_cost_scatter + k_render<true> "
-                                    "(cost-ordered persistent lanes, heavy-pixel coop tiers)")
-                                   if args.spp >= 8 else "rtx_render_rows launch = k_render<false> (exact grid)",
-                         "kernel_ms": round(launch_ms, 4),
-                         "flop_per_launch": flops, "sphere_tests_per_launch": tests_per_launch,
-                         "segments_per_sample": round(st.segments / max(1, st.samples), 4),
-                         "pmc": pmc_note,
-                         "executed": executed},
+            "roofline": roof,
             "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(alg_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
@@ -385,6 +448,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "per_sample_rng": per_sample,
+            "build": build_provenance(rtx),
         }
         print(json.dumps(line), flush=True)
     ctx.close()

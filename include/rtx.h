@@ -40,7 +40,7 @@ extern "C" {
 
 #define RTX_VERSION 130 /* 1.3.0 */
 /* ABI notes.
- *  1.3.0: RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
+ *  1.3.0: rtx_build_info; RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
  *         rtx_stats_reset report a render launch that left pixels unwritten
  *         (the promotion service's safety valve fired) instead of returning
  *         the image as if it were complete.
@@ -139,6 +139,9 @@ typedef struct rtx_ctx rtx_ctx;
 
 /* ---- library / device ------------------------------------------------- */
 RTX_API int rtx_version(void);
+/* Build provenance (1.3.0): "src_sha16=<hash of the sources the library was
+ * compiled from> arch=gfx950" (static string). */
+RTX_API const char *rtx_build_info(void);
 /* Thread-local text of the last failure on this thread ("" if none). */
 RTX_API const char *rtx_last_error(void);
 /* Number of visible HIP devices. */

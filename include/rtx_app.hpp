@@ -63,7 +63,39 @@ struct AppConfig {
     float lens_aperture = 0.0f;            // > 0: thin lens (extension, §8f-3); 0 = reference pinhole
     uint32_t rng_mode = RTX_RNG_CHAIN;
     bool lambert_guard = false;            // RTX_FRAME_LAMBERT_GUARD (extension, §8f-4); false = reference
+    // Drive the library through the reference's own cbuffer bytes: LoadContent
+    // fills a WorldDef (random_world, at most 512 spheres) and hands it to
+    // rtx_world_from_worlddef; Update fills a PerFrame and hands it to
+    // rtx_frame_from_perframe — DxCSApp's data path byte for byte.
+    bool cbuffers = false;
 };
+
+// The reference's constant-buffer byte layouts (HLSL packing: float4 rows).
+// WorldDef, DxCSApp.cpp:64-71: sceneValues {count, depth, spp, -1};
+// spheres[512] (centre, radius); matTypes[128], four codes per float4
+// (SetFloat4Cmpt, :11-17); matValues[512].
+struct WorldDefBytes {
+    float scene_values[4];
+    float spheres[512][4];
+    float mat_types[128][4];
+    float mat_values[512][4];
+};
+static_assert(sizeof(WorldDefBytes) == 18448, "WorldDef is 18,448 bytes");
+// PerFrame, DxCSApp.cpp:30-37: time, perspectiveVals {vfov, aspect,
+// aperture, width}, currSamples, viewVals (4x4, stored transposed, :60).
+struct PerFrameBytes {
+    float time[4];
+    float perspective_vals[4];
+    float curr_samples[4];
+    float view_vals[16];
+};
+static_assert(sizeof(PerFrameBytes) == 112, "PerFrame is 112 bytes");
+// WorldDef::random_world into the cbuffer layout (DxCSApp.cpp:72-134); false
+// if the scene does not fit its 512 slots.
+bool fill_worlddef(const AppConfig &cfg, WorldDefBytes &out);
+// DxCSApp::Update's PerFrame (DxCSApp.cpp:481-492): perspectiveVals,
+// ComputeViewVals with focus_dist = |camPos - camLookAt|, currSamples.
+bool fill_perframe(const AppConfig &cfg, float sample_count, PerFrameBytes &out);
 
 class RtxCSApp : public RtxBase {
 public:

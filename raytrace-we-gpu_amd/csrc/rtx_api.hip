@@ -171,6 +171,15 @@ extern "C" {
 
 int rtx_version(void) { return RTX_VERSION; }
 
+#ifndef RTX_SRC_SHA
+#define RTX_SRC_SHA "unknown"
+#endif
+// Build provenance: the hash of the sources this library was compiled from
+// (Makefile SRC_SHA: sha256 over csrc/* and include/rtx.h, first 16 hex
+// digits) and the offload target, so a run can show that the library it
+// loaded is the one its tree's sources build.
+const char *rtx_build_info(void) { return "src_sha16=" RTX_SRC_SHA " arch=gfx950"; }
+
 const char *rtx_last_error(void) { return g_last_error.c_str(); }
 
 int rtx_device_count(int *count) {

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 
 namespace rtx {
 
@@ -34,9 +35,65 @@ void RtxBase::Terminate() {
 
 RtxCSApp::RtxCSApp(const AppConfig &cfg) : m_cfg(cfg) {}
 
+bool fill_worlddef(const AppConfig &cfg, WorldDefBytes &out) {
+    std::memset(&out, 0, sizeof(out));
+    float sph[4 * 512], mt[512], mv[4 * 512];
+    uint32_t n = 0;
+    if (rtx_scene_random_world(cfg.grid_half_extent, 512, sph, mt, mv, &n) != RTX_OK) return false;
+    const uint64_t full = 4ull + 4ull * (uint64_t)cfg.grid_half_extent * cfg.grid_half_extent;
+    if (full > 512) return false;  // the cbuffer holds 512 spheres (DxCSApp.cpp:67)
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 4; ++k) {
+            out.spheres[i][k] = sph[4 * i + k];
+            out.mat_values[i][k] = mv[4 * i + k];
+        }
+        out.mat_types[i / 4][i % 4] = mt[i];  // SetFloat4Cmpt(matTypes[i/4], i%4, .)
+    }
+    out.scene_values[0] = (float)n;  // { count, 50, 60, -1 } (:133)
+    out.scene_values[1] = (float)cfg.depth;
+    out.scene_values[2] = (float)cfg.spp;
+    out.scene_values[3] = -1.0f;
+    return true;
+}
+
+bool fill_perframe(const AppConfig &cfg, float sample_count, PerFrameBytes &out) {
+    std::memset(&out, 0, sizeof(out));
+    const float persp[4] = {cfg.vfov, cfg.aspect, cfg.aperture, (float)cfg.width};  // :179
+    rtx_frame f{};
+    // ComputeViewVals(camPos, camLookAt, upDir, vfov, aspect, aperture, focus_dist) (:488-489)
+    if (rtx_camera_look_at(cfg.cam_pos, cfg.cam_look_at, cfg.up, persp[0], persp[1], persp[2], 0.0f, cfg.width,
+                           cfg.height, &f) != RTX_OK)
+        return false;
+    std::memcpy(out.perspective_vals, persp, sizeof(persp));
+    const float *rows[4] = {f.origin, f.horizontal, f.vertical, f.lower_left};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) out.view_vals[4 * j + i] = rows[i][j];  // XMMatrixTranspose (:60)
+    for (int k = 0; k < 4; ++k) out.curr_samples[k] = sample_count;       // (:491-492)
+    return true;
+}
+
 RtxCSApp::~RtxCSApp() { Terminate(); }
 
 bool RtxCSApp::LoadContent() {
+    if (m_cfg.cbuffers) {  // the reference's WorldDef bytes through the adapter
+        WorldDefBytes wd;
+        rtx_world w{};
+        m_spheres.assign(4 * 512, 0.0f);
+        m_mat_types.assign(512, 0.0f);
+        m_mat_values.assign(4 * 512, 0.0f);
+        if (m_cfg.scene != SceneKind::RandomWorld || !fill_worlddef(m_cfg, wd) ||
+            rtx_world_from_worlddef(&wd, sizeof(wd), m_spheres.data(), m_mat_types.data(), m_mat_values.data(),
+                                    &w) != RTX_OK) {
+            m_error = "WorldDef: only random_world scenes of at most 512 spheres fit the cbuffer";
+            return m_ok = false;
+        }
+        m_count = w.count;
+        if (rtx_upload_world(m_ctx, &w) != RTX_OK) {  // CreateBuffer(WorldDef, IMMUTABLE) (:393-413)
+            m_error = rtx_last_error();
+            return m_ok = false;
+        }
+        return m_ok = true;
+    }
     // WorldDef w; WorldDef::random_world(w);  (DxCSApp.cpp:401-402)
     uint32_t cap = m_cfg.scene == SceneKind::PsWorld ? 7 : 4;
     if (m_cfg.scene == SceneKind::RandomWorld) {
@@ -83,7 +140,12 @@ void RtxCSApp::Update() {
     // focus_dist = |camPos - camLookAt|; ComputeViewVals; sampleCount++
     // (DxCSApp.cpp:488-492), then the PerFrame upload (:494-496).
     int rc;
-    if (m_cfg.simple_camera)
+    if (m_cfg.cbuffers) {  // the reference's PerFrame bytes through the adapter
+        PerFrameBytes pf;
+        rc = fill_perframe(m_cfg, (float)(m_frame_count + 1), pf)
+                 ? rtx_frame_from_perframe(&pf, sizeof(pf), m_cfg.width, m_cfg.height, &m_frame)
+                 : RTX_ERR_INVALID;
+    } else if (m_cfg.simple_camera)
         rc = rtx_camera_simple(m_cfg.width, m_cfg.height, &m_frame);
     else
         rc = rtx_camera_look_at(m_cfg.cam_pos, m_cfg.cam_look_at, m_cfg.up, m_cfg.vfov, m_cfg.aspect,

@@ -7,10 +7,15 @@
 //           [--scene rtiow9|rtiow11|test|ps|random:EXT[:MAX]] [--simple-camera]
 //           [--rng chain|per-sample] [--frames K] [--device N]
 //           [--aperture A] [--accumulate] [--lambert-guard]
-//           [--pfm out.pfm] [--ppm out.ppm]
+//           [--reference-frame] [--pfm out.pfm] [--ppm out.ppm]
 // --accumulate renders the K frames progressively (rtx_accumulate) instead
 // of K independent frames; --aperture enables the thin lens;
 // --lambert-guard the near-zero diffuse guard (RTX_FRAME_LAMBERT_GUARD).
+// --reference-frame: the reference's frame as shipped — 1024x576, spp 60,
+// depth 50, random_world with 326 spheres, camera (13,2,3) -> 0, vfov 20,
+// aspect 16/9 (DxCSApp.cpp:133,176-179,330-331) — uploaded as the reference's
+// own WorldDef and PerFrame cbuffer bytes through rtx_world_from_worlddef /
+// rtx_frame_from_perframe (later options still override).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -25,7 +30,8 @@ static void usage() {
                  "usage: rtx_cli [--width W] [--height H] [--spp S] [--depth D]\n"
                  "               [--scene rtiow9|rtiow11|test|ps|random:EXT[:MAX]] [--simple-camera]\n"
                  "               [--rng chain|per-sample] [--frames K] [--device N]\n"
-                 "               [--aperture A] [--accumulate] [--lambert-guard] [--pfm FILE] [--ppm FILE]\n");
+                 "               [--aperture A] [--accumulate] [--lambert-guard] [--reference-frame]\n"
+                 "               [--pfm FILE] [--ppm FILE]\n");
 }
 
 int main(int argc, char **argv) {
@@ -59,6 +65,10 @@ int main(int argc, char **argv) {
         else if (a == "--aperture") cfg.lens_aperture = (float)std::atof(next());
         else if (a == "--accumulate") accumulate = true;
         else if (a == "--lambert-guard") cfg.lambert_guard = true;
+        else if (a == "--reference-frame") {
+            cfg = rtx::AppConfig();  // the reference's values (include/rtx_app.hpp)
+            cfg.cbuffers = true;
+        }
         else if (a == "--rng") {
             const std::string m = next();
             cfg.rng_mode = (m == "per-sample") ? RTX_RNG_PER_SAMPLE : RTX_RNG_CHAIN;
@@ -120,9 +130,10 @@ int main(int argc, char **argv) {
     rtx_stats st{};
     rtx_get_stats(app.context(), &st);
     std::printf("{\"width\": %u, \"height\": %u, \"spp\": %u, \"depth\": %u, \"spheres\": %u, "
-                "\"frames\": %d, \"wall_s\": %.6f, \"kernel_ms\": %.4f, \"msamples_per_s\": %.3f, "
+                "\"cbuffers\": %s, \"frames\": %d, \"wall_s\": %.6f, \"kernel_ms\": %.4f, \"msamples_per_s\": %.3f, "
                 "\"segments\": %llu, \"sphere_tests\": %llu}\n",
-                cfg.width, cfg.height, cfg.spp, cfg.depth, app.sphere_count(), frames, wall,
+                cfg.width, cfg.height, cfg.spp, cfg.depth, app.sphere_count(), cfg.cbuffers ? "true" : "false",
+                frames, wall,
                 st.kernel_ms, (double)st.samples / wall / 1e6, (unsigned long long)st.segments,
                 (unsigned long long)st.sphere_tests);
     if (!pfm.empty() || !ppm.empty()) {

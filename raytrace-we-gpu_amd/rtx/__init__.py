@@ -93,6 +93,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     ctx = C.c_void_p
     sig = {
         "rtx_version": (C.c_int, []),
+        "rtx_build_info": (C.c_char_p, []),
         "rtx_last_error": (C.c_char_p, []),
         "rtx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
         "rtx_create": (C.c_int, [C.c_int, C.POINTER(ctx)]),
@@ -136,7 +137,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     }
     # entry points added after 1.0 may be absent from older builds (A/B runs
     # of earlier libraries); calling one then fails with AttributeError
-    optional = {"rtx_schedule_defaults", "rtx_set_schedule", "rtx_get_schedule", "rtx_debug_hit_world_from"}
+    optional = {"rtx_schedule_defaults", "rtx_set_schedule", "rtx_get_schedule", "rtx_debug_hit_world_from",
+                "rtx_build_info"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(lib, name):
             continue
@@ -274,6 +276,15 @@ def schedule_defaults() -> rtx_schedule:
     sch = rtx_schedule()
     _check(lib.rtx_schedule_defaults(C.byref(sch)), "rtx_schedule_defaults")
     return sch
+
+
+def build_info(lib: Optional[C.CDLL] = None) -> dict:
+    """rtx_build_info of the loaded library: {"src_sha16": ..., "arch": ...}
+    (empty for libraries older than ABI 1.3)."""
+    lib = lib or load_library()
+    if not hasattr(lib, "rtx_build_info"):
+        return {}
+    return dict(kv.split("=", 1) for kv in lib.rtx_build_info().decode().split())
 
 
 def device_count() -> int:

@@ -3,6 +3,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -169,3 +170,14 @@ def test_schedule_calls_refuse_an_older_abi(rtx):
     with pytest.raises(rtx.RtxError, match="predates"):
         rtx._require_schedule_abi(OldLib())
     rtx._require_schedule_abi(rtx.load_library())  # the in-tree library passes
+
+
+def test_library_built_from_this_tree(rtx):
+    """Build provenance: the library's embedded source hash (rtx_build_info,
+    Makefile SRC_SHA) equals the hash of the tree's sources, i.e. the loaded
+    librtx.so was compiled from exactly these files."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from src_sha import src_sha16
+    info = rtx.build_info()
+    assert info.get("arch") == "gfx950"
+    assert info.get("src_sha16") == src_sha16(), "librtx.so is stale: rebuild (make)"

@@ -352,6 +352,30 @@ def test_c5_full_width_rows(gpu_ctx, oracle, rtx):
     assert int(cost[rows].sum(dtype=np.uint64)) == segs
 
 
+def test_per_sample_c5_full_width_rows(gpu_ctx, oracle, rtx):
+    """C5 at full size in per-sample RNG mode (rng_mode 1: 1920x1080, 100k
+    spheres, spp 16, depth 50) — the path where round 3's illegal-address
+    fault hit ("Faults"): k_render_ps with the kPF SGPR scan
+    (no per-wave LDS tile in this kernel) and its group-coop tail reading the
+    scene from HBM. Two full rows bit-exact against the oracle in the same
+    RNG mode; the frame's segment count equal to an independent exact-grid
+    pass's per-pixel counts (rtx_debug_pixel_cost, per-sample seeds too),
+    whose sums over those rows equal the oracle's."""
+    W, H = 1920, 1080
+    world = rtx.random_world(159, capacity=100000, depth=50, spp=16)
+    frame = rtx.camera_look_at(W, H)
+    frame.rng_mode = 1
+    img, st = render_gpu(gpu_ctx, world, frame)
+    assert st.samples == W * H * 16
+    rows = np.array([211, 866], np.uint32)
+    want, segs = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img[rows], want, "per-sample C5 rows")
+    assert np.isfinite(img).all()
+    cost = gpu_ctx.debug_pixel_cost(0)
+    assert int(cost.sum(dtype=np.uint64)) == st.segments
+    assert int(cost[rows].sum(dtype=np.uint64)) == segs
+
+
 def test_edge_cases(gpu_ctx, oracle, rtx):
     """Empty scene (all sky), spp 0 (0/0 = NaN, as accColor /= 0), depth 0
     (black), unknown material code (no scatter -> black), 1x1 frame."""
@@ -843,6 +867,46 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
     ctx.set_schedule()
 
 
+def test_promotion_across_the_chip(gpu_ctx, oracle, rtx):
+    """Promotion with every workgroup of the chip taking part: a
+    1280x720 frame (2.8 pixels per resident lane: a "medium" part) with
+    promote_* 1 — nearly every pixel still in flight once the queue is empty
+    is handed over, the 65,536-entry queue overflows — and k_trace beside the
+    render (trace_* 0.3, the combination whose exit used to depend on both
+    kernels running together). Entries cross XCDs (the queue is one array;
+    producers and servers sit on all 8). The launch must complete (no
+    RTX_ERR_INCOMPLETE from rtx_get_stats), rows bit-exact, and the segment
+    count equal to an independent exact-grid pass's."""
+    W, H, T = 1280, 720, 5
+    world = rtx.random_world(11, depth=50, spp=12)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(frame)
+    rows = np.linspace(2, H - 3, 6).astype(np.uint32)
+    want, segs_rows = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    cost = gpu_ctx.debug_pixel_cost(0)
+    assert int(cost[rows].sum(dtype=np.uint64)) == segs_rows
+    for sched in (dict(promote_small=1, promote_low=1, promote_medium=1, promote_large=1),
+                  dict(promote_small=1, promote_low=1, promote_medium=1, promote_large=1, trace_small=0.3,
+                       trace_low=0.3, trace_medium=0.3, trace_large=0.3, tier1_bar=1.2, tier1_bar_small=1.5,
+                       tier1_bar_low=1.5)):
+        gpu_ctx.set_schedule()
+        gpu_ctx.set_schedule(**sched)
+        for nparts, part in ((1, 0), (2, 1)):
+            ids = rtx.part_row_ids(H, T, part, nparts)
+            buf = gpu_ctx.alloc((len(ids), W, 4))
+            gpu_ctx.stats_reset()
+            gpu_ctx.render_rows(T, part, nparts, buf.ptr)
+            st = gpu_ctx.stats()  # raises RtxError (RTX_ERR_INCOMPLETE) if pixels were left unwritten
+            got = buf.numpy()
+            buf.free()
+            assert st.segments == int(cost[ids].sum(dtype=np.uint64)), f"{sched} part {part} of {nparts}"
+            mine = np.isin(rows, ids)
+            pos = np.searchsorted(ids, rows[mine])
+            assert_bits_equal(got[pos], want[mine], f"{sched} part {part} of {nparts}")
+    gpu_ctx.set_schedule()
+
+
 @pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
 def test_promotion_large_scene_bit_exact(request, oracle, rtx, ctx_name):
     """Promotion in the large-scene (kPF) kernels, where the promoted pixel's
@@ -991,6 +1055,36 @@ def test_cli_writes_reference_frame(tmp_path, oracle, rtx):
         img8 = np.frombuffer(f.read(), np.uint8).reshape(36, 64, 3)
     v = np.nan_to_num(want[::-1, :, :3], nan=0.0)
     np.testing.assert_array_equal(img8, (np.float32(255.999) * np.clip(v, 0, 1).astype(np.float32)).astype(np.uint8))
+
+
+def test_reference_frame_through_cbuffer_bytes(tmp_path, oracle, rtx):
+    """The drop-in on the reference's own bytes: rtx_cli
+    --reference-frame fills WorldDef (18,448 B) and PerFrame (112 B) as
+    DxCSApp does (DxCSApp.cpp:39-61, 72-134, 481-496), hands them to
+    rtx_world_from_worlddef / rtx_frame_from_perframe, and renders the frame
+    as shipped: 1024x576, spp 60, depth 50, 326 spheres (:133, :179,
+    :330-331, Dispatch :524). Eight full rows bit-exact against the oracle's
+    render of the same scene and camera."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "raytrace-we-gpu_amd", "bin", "rtx_cli")
+    pfm = str(tmp_path / "ref.pfm")
+    out = subprocess.run([cli, "--reference-frame", "--frames", "1", "--pfm", pfm],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    rep = __import__("json").loads(out.stdout.strip().splitlines()[-1])
+    assert (rep["width"], rep["height"], rep["spp"], rep["depth"], rep["spheres"], rep["cbuffers"]) == \
+        (1024, 576, 60, 50, 326, True)
+    with open(pfm, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        assert (w, h) == (1024, 576) and float(f.readline()) < 0
+        img = np.frombuffer(f.read(), "<f4").reshape(h, w, 3)
+    world = rtx.random_world(9, depth=50, spp=60)
+    frame = rtx.camera_look_at(1024, 576, aspect=16.0 / 9.0)
+    rows = np.linspace(3, 572, 8).astype(np.uint32)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(img[rows], want[..., :3], "reference frame rows")
+    assert np.isfinite(img).all()
 
 
 def test_upload_rejects_out_of_range_scene(gpu_ctx, rtx):
