@@ -40,7 +40,9 @@ extern "C" {
 
 #define RTX_VERSION 130 /* 1.3.0 */
 /* ABI notes.
- *  1.3.0: rtx_build_info; RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
+ *  1.3.0: rtx_schedule.trace_solo_bar (after promote_big_scene) and
+ *         trace_group (after refill_chunk): the struct grew by 8 bytes;
+ *         rtx_build_info; RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
  *         rtx_stats_reset report a render launch that left pixels unwritten
  *         (the promotion service's safety valve fired) instead of returning
  *         the image as if it were complete.
@@ -190,7 +192,11 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *   - trace_*: for scenes up to 640 spheres tier 1 runs in its own kernel
  *     beside the render (one pixel per wave, all 64 lanes on its ray), with
  *     this fraction of the resident waves for a small / low / medium /
- *     larger part (0: tier 1 stays in the render kernel);
+ *     larger part (0: tier 1 stays in the render kernel); trace_group
+ *     pixels per wave of it (each traced by 64 / trace_group lanes: more
+ *     chains for about the same issue, a little longer per segment), except
+ *     keys above trace_solo_bar x share, traced one per wave; the kernel also
+ *     serves the promotion queue once tier 1 is done;
  *   - promote_*: once the pixel queue is empty, a lane whose pixel is
  *     projected to need more than this many further ray segments hands it
  *     over at a sample boundary to a wave with nothing else to do (an idle
@@ -230,12 +236,15 @@ typedef struct rtx_schedule {
     float promote_medium;     /* default 500 */
     float promote_large;      /* default 400 */
     float promote_big_scene;  /* default 60: every part of a scene above 640 spheres */
+    float trace_solo_bar;     /* default 1e30 (none): tier-1 keys above this x share are traced one pixel
+                                 per wave even when trace_group > 1 */
     uint32_t tail_coop_max;   /* default 32 */
     uint32_t tail_coop_max_large; /* default 8: the same for scenes above 640 spheres */
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
     uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
+    uint32_t trace_group;     /* default 1: tier-1 pixels per wave of the tier-1 kernel (1, 2, 4, 8, 16) */
     uint32_t reserved;        /* must be 0 */
 } rtx_schedule;
 /* The library's defaults (no context, no GPU). */
@@ -244,7 +253,8 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
  * tail_coop_max and tail_coop_max_large in 1..64,
- * priorities in 0..3, refill_chunk in 0..4096, reserved 0. */
+ * priorities in 0..3, refill_chunk in 0..4096, trace_group a power of two
+ * in 1..16, trace_solo_bar > 0, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 

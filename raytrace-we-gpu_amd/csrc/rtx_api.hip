@@ -295,6 +295,8 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
     out->refill_chunk = t.chunk;
+    out->trace_group = t.trace_group;
+    out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
     return RTX_OK;
 }
 
@@ -308,7 +310,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         {"tier1_bar", s->tier1_bar},         {"tier1_bar_small", s->tier1_bar_small},
         {"tier1_bar_low", s->tier1_bar_low}, {"tier2_bar_small", s->tier2_bar_small},
         {"tier2_bar_medium", s->tier2_bar_medium}, {"tier2_bar", s->tier2_bar}, {"small_share", s->small_share},
-        {"low_share", s->low_share},         {"medium_share", s->medium_share}};
+        {"low_share", s->low_share},         {"medium_share", s->medium_share},
+        {"trace_solo_bar", s->trace_solo_bar}};
     for (const auto &f : pos)
         if (!(f.v > 0.0f && f.v <= 1e30f))
             return fail(RTX_ERR_INVALID, std::string("rtx_set_schedule: ") + f.name + " must be finite and > 0");
@@ -330,6 +333,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     if (s->tier1_priority > 3 || s->tier2_priority > 3 || s->hot_priority > 3)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: priorities must be in 0..3");
     if (s->refill_chunk > 4096) return fail(RTX_ERR_INVALID, "rtx_set_schedule: refill_chunk must be in 0..4096");
+    if (s->trace_group < 1 || s->trace_group > 16 || (s->trace_group & (s->trace_group - 1)) != 0)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_group must be 1, 2, 4, 8 or 16");
     if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
     rtx::KTune t;
     t.a1 = s->tier1_bar;
@@ -360,6 +365,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.prio_t2 = s->tier2_priority;
     t.prio_hot = s->hot_priority;
     t.chunk = s->refill_chunk;
+    t.trace_group = s->trace_group;
+    t.trace_solo = s->trace_solo_bar;
     c->tune = t;
     return RTX_OK;
 }
@@ -396,6 +403,8 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->tier2_priority = t.prio_t2;
     out->hot_priority = t.prio_hot;
     out->refill_chunk = t.chunk;
+    out->trace_group = t.trace_group;
+    out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
     return RTX_OK;
 }
 
@@ -541,9 +550,9 @@ uint32_t rtx_part_rows(uint32_t height, uint32_t tile_rows, uint32_t part, uint3
 static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out,
                        float4 *accum, uint32_t accum_frames, uint32_t frame_index);
 
-// Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + 4], then the
+// Scheduling scratch (words): cost[npix] perm[npix] buckets[2K + kSchedWords], then the
 // per-pixel pre-pass state (float4, 16-byte aligned).
-static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + 8 + 3) & ~(size_t)3; }
+static size_t sched_state_off(size_t npix) { return (2 * npix + 2 * rtx::kCostBuckets + rtx::kSchedWords + 3) & ~(size_t)3; }
 constexpr uint32_t kPromCap = 65536;  // promotion queue entries (8 words each)
 
 int rtx_render_rows(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t nparts, void *d_out) {

@@ -78,11 +78,13 @@ struct KParams {
     // promotion (k_trace beside k_render): once its queue is empty, a lane-mode
     // wave hands a pixel whose projected remaining segments exceed prom_min
     // to k_trace at a sample boundary (rtx_kernels.hip, promote)
-    uint32_t *prom;                // [0] entries claimed [1] entries taken [2] k_render-owned pixels written; NULL: off
+    uint32_t *prom;                // [0] entries claimed [1] entries taken [2] k_render-owned pixels written
+                                   // [3] k_render workgroups started; NULL: off
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
-    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 (NULL = none)
+    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0 (NULL = none)
+    uint32_t trace_lg;             // k_trace: log2(lanes per pixel) of its waves past the solo slots [0, k0)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
     float *ps_scratch;
@@ -108,6 +110,8 @@ struct KTune {
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
     double prom_big;                                           // ... for scenes without the coop's LDS copy
+    uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2, 4, 8)
+    double trace_solo;                                         // ... one per wave above this x share (k0)
 };
 KTune default_tune();
 
@@ -115,7 +119,7 @@ struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
     float4 *state;      // [npix] (acc.xyz, seed) after the pre-pass's samples
-    uint32_t *buckets;  // [2 * nbuckets + 4]: counts, cursors, heavy counters and ends (zeroed per launch)
+    uint32_t *buckets;  // [2 * nbuckets + kSchedWords]: counts, cursors, heavy[8], prom[8] (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object
     float *ps_scratch;  // k_render_ps scratch (rng_mode 1), ps_floats floats
@@ -128,6 +132,9 @@ struct KSchedule {
     uint32_t epoch;     // launch counter: a promotion entry is ready when its last word equals it
 };
 constexpr uint32_t kCostBuckets = 256;
+// Scheduling words after the two bucket arrays (counts, cursors), zeroed per
+// launch: heavy[8] (KParams::heavy), then prom[8] (KParams::prom).
+constexpr uint32_t kSchedWords = 16;
 #ifndef RTX_COST_SPP
 #define RTX_COST_SPP 2
 #endif

@@ -113,6 +113,10 @@ constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLar
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
+// k_trace: tier-1 pixels per wave (1, 2, 4, 8), and the key bar (x share)
+// above which a pixel is traced alone in its wave nonetheless
+constexpr uint32_t kTraceGroup = 1;
+constexpr double kTraceSolo = 1e30;
 // Cost pre-pass cap (whole-frame parts only: in a row-split share a capped,
 // under-rated key keeps heavy pixels out of the tiers — parts 2/4/8 30/21/15
 // -> 34/26/26 ms, profiles/R4h_parts.jsonl): a pixel still tracing after
@@ -864,6 +868,9 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
     return active ? result : -1;
 }
 
+#ifndef RTX_PROM_EXACT_RATE  // A/B: a restarted pixel's promotion rate over its samples from 0 (1) or from cost_spp (0)
+#define RTX_PROM_EXACT_RATE 1
+#endif
 // Lane state: the pixel it is tracing and that pixel's current path.
 constexpr uint32_t kSeg0Restart = 0x80000000u;  // Lane::seg0 flag (a lane's segs stay far below 2^31)
 struct Lane {
@@ -1130,7 +1137,7 @@ __device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
     // samples traced in this launch (>= 1 here): after the pre-pass's
     // cost_spp, or from sample 0 for a pixel the pre-pass stopped (cost_cap;
     // kSeg0Restart in seg0)
-    const bool restarted = (L.seg0 & kSeg0Restart) != 0u;
+    const bool restarted = RTX_PROM_EXACT_RATE && (L.seg0 & kSeg0Restart) != 0u;
     const uint32_t done = max(restarted ? L.sample : L.sample - min(L.sample, P.cost_spp), 1u);
     const uint32_t segs = L.segs - (L.seg0 & ~kSeg0Restart);
     if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
@@ -1350,112 +1357,145 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
         H.tier = 2;
 }
 
-// ---- one pixel traced by the whole wave: tier 1 (k_trace) -----------------
+// ---- tier 1 traced by groups of lanes (k_trace) ----------------------------
 // A pixel whose chain is the critical path of the frame (or of a rank's
-// share) is traced to its end by all 64 lanes of a wave: every lane holds
-// the same Lane state, lane k scans sphere pairs k, k + 64, ... (the group
-// coop's scan with g = 64, from the LDS copy), the wave reduces (min c, then
-// the largest index among equal c: the in-order scan's answer) and shades
-// uniformly with the lane-mode functions. Taken off each segment's critical
-// path: the scatter's seed-determined part (scatter_spec) is evaluated before
-// the scan, and each lane loads the material of its own best candidate while
-// the wave reduces; the winner's is then read from its lane. A non-finite
-// root takes the exact in-order scan (every lane the same ray). W: the
-// pixel's state after start_pixel, the same in every lane; on return the
-// pixel's samples are done (W.acc, W.seed, W.segs final).
+// share) is traced to its end by a group of g = 2^lg lanes of a wave (lg 6:
+// the whole wave), every lane of the group holding the same Lane state: lane
+// k of the group scans sphere pairs k, k + g, ... (the group coop's scan,
+// from the LDS copy), the group reduces (min c, then the largest index among
+// equal c: the in-order scan's answer) and shades uniformly with the
+// lane-mode functions. Taken off each segment's critical path: the scatter's
+// seed-determined part (scatter_spec) is evaluated before the scan, and each
+// lane loads the material of its own best candidate while the group reduces;
+// the winner's is then read from its lane. A non-finite root takes the exact
+// in-order scan (the group's lanes, the same ray). Several groups per wave
+// trace several chains for little more issue than one: the scan's pairs are
+// split over fewer lanes, everything else is issued once for all groups.
+// One segment of every active group (the group's lanes hold its pixel's
+// state W; lanes of groups without a pixel flag nothing); `ended`: the
+// group's pixel finished its last sample (W.acc, W.seed final).
 template <typename Src>
-__device__ __forceinline__ void trace_pixel_uniform(const KParams &P, const Frame &F, const Src &src, Lane &W,
-                                                    unsigned long long *cp, unsigned long long *tq) {
+__device__ __forceinline__ void trace_group_segment(const KParams &P, const Frame &F, const Src &src, uint32_t lg,
+                                                    Lane &W, bool &ended) {
     const KScene &S = P.scene;
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = 1u << lg, k = lane & (g - 1u);
+    const uint64_t gm = lg >= 6u ? ~0ull : ((1ull << g) - 1ull) << (lane & ~(g - 1u));  // my group's lanes
     const float inf = __uint_as_float(0x7f800000u);
     const int last = (int)S.n - 1;
-    const uint32_t plast = src.npairs - 1u;
-    const uint32_t nsteps = (src.npairs + 63u) >> 6;
-    for (;;) {
-        RTX_CP(4)
-        if (RTX_DIAG_COOP && cp) cp[5]++;
-        const ScatterSpec sp = scatter_spec(W.seed);
-        const LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
-        const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
-        const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
-        uint64_t key = hit_key(inf, -1);
-        bool ok = true;
-        RTX_CP(0)
-#pragma unroll 1
-        for (uint32_t s0 = 0; s0 < nsteps; s0 += kGfSteps) {
-            // the group coop's scan and resolve (hit_world_groups) with g = 64
-            uint32_t im = 0;
-            const uint32_t s1 = min(s0 + kGfSteps, nsteps);
-            auto step = [&](uint32_t st) {
-                f2v cx, cy, cz, R;
-                src.pair(Src::kPadded ? (st << 6) + lane : min((st << 6) + lane, plast), cx, cy, cz, R);
-                const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
-                const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
-                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
-                im = (im << 1) | (__float_as_uint(q.y) >> 31);
-                im = (im << 1) | (__float_as_uint(q.x) >> 31);
-            };
-            uint32_t st = s0;
-            for (; st + 2u <= s1; st += 2u) {
-                step(st);
-                step(st + 1u);
-            }
-            if (st < s1) step(st);
-            const uint32_t nb = 2u * (s1 - s0);
-            uint32_t fm = ~im & (nb >= 32u ? ~0u : ((1u << nb) - 1u));
-#pragma unroll 1
-            while (__ballot(fm != 0u) != 0ull) {
-                const bool live = fm != 0u;
-                const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
-                fm &= fm - 1u;
-                const uint32_t p = ((s1 - 1u - (bit >> 1)) << 6) + lane;
-                const uint32_t j = 2u * (Src::kPadded ? p : min(p, plast)) + (bit & 1u);
-                resolve_one(src.sphere(j), (int)j, live, W.o, W.d, W.a, W.inv_a, kTMin, key, ok);
-            }
-        }
-        RTX_CP(1)
-        // each lane's best candidate: its material is loaded during the reduction
-        const uint32_t lo = ~(uint32_t)key;  // index + 1, 0: none
-        const uint32_t jl = lo != 0u ? min(lo - 1u, (uint32_t)last) : 0u;
-        const int mt_l = S.mtype[jl];
-        const float4 mv_l = S.mval[jl];
-        const uint32_t cb0 = (uint32_t)(key >> 32);
-        const uint32_t cb = group_reduce_u32<false>(cb0, 6u);
-        const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? lo : 0u, 6u);
-        int hit = -1;
-        float t = inf;
-        HitMat M;
-        if (__ballot(!ok) != 0ull) {  // a non-finite root: the exact in-order scan
-            hit = hit_blocks_seq((cfloat_p)S.soa, S.n_pad / 8u, 0, W.o, W.d, W.a, W.inv_a, kTMin, t, -1);
-            if (hit >= 0) {
-                hit = min(hit, last);
-                M = hit_mat(S, hit);
-            }
-        } else if (ib != 0u) {
-            hit = min((int)(ib - 1u), last);
-            t = __uint_as_float(cb);
-            const int wl = __builtin_ctzll(__ballot(lo == ib && cb0 == cb));  // a lane holding the winner
-            M.sc = src.sphere((uint32_t)hit);  // the same floats as cen[hit]
-            M.mt = __builtin_amdgcn_readlane(mt_l, wl);
-            M.mv = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.x), wl)),
-                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.y), wl)),
-                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.z), wl)),
-                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.w), wl)));
-        }
-        RTX_CP(2)
-        W.segs++;
-        f3 c;
-        const int r = path_segment_m<true>(P, W, hit, t, M, sp, c);
-        if (r == kSegSky) W.acc = W.acc + c;
-        if (r != kSegContinue) {
-            W.sample++;
-            if (W.sample >= P.spp) break;
-            begin_sample(P, F, W.x, W.y, W);
-        }
-        RTX_CP(3)
+    const ScatterSpec sp = scatter_spec(W.seed);
+    LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
+    if (!W.active) {  // no pixel: nothing is flagged
+        T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
+        T.thr = inf;
     }
-    RTX_CP(3)
+    const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
+    uint64_t key = hit_key(inf, -1);
+    bool ok = true;
+    const uint32_t nsteps = src.npairs >> lg;  // SphLds: npairs is a multiple of 64
+#pragma unroll 1
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += kGfSteps) {
+        // the group coop's scan and resolve (hit_world_groups)
+        uint32_t im = 0;
+        const uint32_t s1 = min(s0 + kGfSteps, nsteps);
+        auto step = [&](uint32_t st) {
+            f2v cx, cy, cz, R;
+            src.pair((st << lg) + k, cx, cy, cz, R);
+            const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+            const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
+            const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
+            im = (im << 1) | (__float_as_uint(q.y) >> 31);
+            im = (im << 1) | (__float_as_uint(q.x) >> 31);
+        };
+        uint32_t st = s0;
+        for (; st + 2u <= s1; st += 2u) {
+            step(st);
+            step(st + 1u);
+        }
+        if (st < s1) step(st);
+        const uint32_t nb = 2u * (s1 - s0);
+        uint32_t fm = ~im & (nb >= 32u ? ~0u : ((1u << nb) - 1u));
+#pragma unroll 1
+        while (__ballot(fm != 0u) != 0ull) {
+            const bool live = fm != 0u;
+            const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
+            fm &= fm - 1u;
+            const uint32_t p = ((s1 - 1u - (bit >> 1)) << lg) + k;
+            const uint32_t j = 2u * p + (bit & 1u);
+            resolve_one(src.sphere(j), (int)j, live, W.o, W.d, W.a, W.inv_a, kTMin, key, ok);
+        }
+    }
+    // each lane's best candidate: its material is loaded during the reduction
+    const uint32_t lo = ~(uint32_t)key;  // index + 1, 0: none
+    const uint32_t jl = lo != 0u ? min(lo - 1u, (uint32_t)last) : 0u;
+    const int mt_l = S.mtype[jl];
+    const float4 mv_l = S.mval[jl];
+    const uint32_t cb0 = (uint32_t)(key >> 32);
+    const uint32_t cb = group_reduce_u32<false>(cb0, lg);
+    const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? lo : 0u, lg);
+    const uint64_t win = __ballot(ib != 0u && lo == ib && cb0 == cb) & gm;  // lanes holding the group's winner
+    const uint64_t bad = __ballot(!ok) & gm;                               // a non-finite root in the group
+    // the winner's material from its lane (every lane takes part in the permutes)
+    const int wl = win != 0ull ? (int)__builtin_ctzll(win) : (int)lane;
+    HitMat M;
+    M.mt = __shfl(mt_l, wl, 64);
+    M.mv = make_float4(__shfl(mv_l.x, wl, 64), __shfl(mv_l.y, wl, 64), __shfl(mv_l.z, wl, 64),
+                       __shfl(mv_l.w, wl, 64));
+    ended = false;
+    if (!W.active) return;
+    int hit = -1;
+    float t = inf;
+    if (bad != 0ull) {  // the exact in-order scan, the group's ray in every lane of it
+        hit = hit_blocks_seq((cfloat_p)S.soa, S.n_pad / 8u, 0, W.o, W.d, W.a, W.inv_a, kTMin, t, -1);
+        if (hit >= 0) {
+            hit = min(hit, last);
+            M = hit_mat(S, hit);
+        }
+    } else if (ib != 0u) {
+        hit = min((int)(ib - 1u), last);
+        t = __uint_as_float(cb);
+        M.sc = src.sphere((uint32_t)hit);  // the same floats as cen[hit]
+    }
+    W.segs++;
+    f3 c;
+    const int r = path_segment_m<true>(P, W, hit, t, M, sp, c);
+    if (r == kSegSky) W.acc = W.acc + c;
+    if (r != kSegContinue) {
+        W.sample++;
+        if (W.sample >= P.spp) {
+            ended = true;
+            return;
+        }
+        begin_sample(P, F, W.x, W.y, W);
+    }
+}
+
+// Move the wave's pixels into fewer, larger groups: the n-th active group of
+// lg (n < m active groups) becomes group n of nlg — every lane of the new
+// group copies the Lane state of a lane of the old one (all lanes of a group
+// hold the same state); new groups past m are idle.
+__device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint64_t act) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t lead = 0;  // the first lane of every active group
+    for (uint32_t r = 0; r < (64u >> lg); ++r)
+        if ((act >> (r << lg)) & 1ull) lead |= 1ull << (r << lg);
+    const uint32_t m = (uint32_t)__popcll(lead);
+    const uint32_t rn = lane >> nlg;
+    uint64_t mm = lead;
+    for (uint32_t i = 0; i < rn && mm != 0ull; ++i) mm &= mm - 1ull;
+    const bool has = rn < m;
+    const int src = has ? (int)__builtin_ctzll(mm) : (int)lane;
+    auto mvf = [src](float &v) { v = __shfl(v, src, 64); };
+    auto mvu = [src](uint32_t &v) { v = (uint32_t)__shfl((int)v, src, 64); };
+    mvf(W.o.x); mvf(W.o.y); mvf(W.o.z);
+    mvf(W.d.x); mvf(W.d.y); mvf(W.d.z);
+    mvf(W.col.x); mvf(W.col.y); mvf(W.col.z);
+    mvf(W.acc.x); mvf(W.acc.y); mvf(W.acc.z);
+    mvf(W.a); mvf(W.inv_a); mvf(W.seed);
+    mvu(W.sample); mvu(W.bounce); mvu(W.segs);
+    mvu(W.x); mvu(W.y); mvu(W.gid); mvu(W.slot); mvu(W.seg0);
+    W.active = has;
 }
 
 // Promotion queue service: wait for an entry and load it into W (every lane
@@ -1685,14 +1725,98 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     }
 }
 
+// Promotion service for the idle groups of a k_trace wave (`need`: the first
+// lane of every idle group of size 2^lg): claims up to one entry per idle
+// group in one CAS and loads each into its group's lanes (take_promoted's
+// protocol and exit rule, k_trace's `helper` side). Returns the entries
+// claimed, or -1 once the service is over for this wave: every pixel k_render
+// owns is written, k_render has not started, or the valve fired. `blocking`
+// (the wave has nothing else to trace): poll until an entry or the end;
+// otherwise one look.
+__device__ __forceinline__ int take_promoted_groups(const KParams &P, const Frame &F, uint32_t npix, uint32_t target,
+                                                    uint64_t need, uint32_t lg, bool blocking, Lane &W) {
+    const uint32_t lane = threadIdx.x & 63u;
+    auto ld = [](const uint32_t *p) {
+        return (uint32_t)__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t seen = ~0u;
+    const uint32_t nneed = (uint32_t)__popcll(need);
+    // this lane's group among the idle ones (only meaningful in idle groups)
+    const uint32_t rank = (uint32_t)__popcll(need & ((1ull << (lane & ~((1u << lg) - 1u))) - 1ull));
+    for (;;) {
+        const uint32_t done = ld(&P.prom[2]);
+        if (done >= target || ld(&P.prom[3]) == 0u) return -1;
+        if (done != seen) {
+            seen = done;
+            t0 = __builtin_amdgcn_s_memrealtime();
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const uint32_t t = min(ld(&P.prom[0]), P.prom_cap);
+        const uint32_t h = ld(&P.prom[1]);
+        const uint32_t want = h < t ? min(t - h, nneed) : 0u;
+        if (want != 0u) {
+            uint32_t won = 0;
+            if (lane == 0u) won = atomicCAS(&P.prom[1], h, h + want) == h ? 1u : 0u;
+            won = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)won, 0, 64));
+            if (won == 0u) continue;  // another server took them first
+            bool torn = false;
+            if (!W.active && rank < want) {
+                const uint32_t *e = P.prom_q + 8u * (h + rank);
+                while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) break;
+                }
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the fields are read after the epoch matched
+                W.gid = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                W.sample = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                W.seed = __uint_as_float(__hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                W.acc = mk3(__uint_as_float(__hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                            __uint_as_float(__hip_atomic_load(e + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                            __uint_as_float(__hip_atomic_load(e + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+                const bool late = __hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch;
+                torn = late || W.gid >= npix || W.sample >= P.spp;
+                if (!torn) {
+                    lane_pixel(P, W.gid, W.x, W.y);
+                    W.seg0 = W.segs;
+                    W.slot = ~0u;  // a promoted pixel: counted in prom[2] when written
+                    W.active = true;
+                    begin_sample(P, F, W.x, W.y, W);
+                    diag_pixel_start(P, W.gid, 3ull);
+                }
+            }
+            if (__ballot(torn) != 0ull) {  // never: a late or torn entry ends the wave's service, not the GPU
+                flag_error(P, kErrPromTorn | kErrPromTimeout);
+                W.active = W.active && !torn;
+                return -1;
+            }
+            return (int)want;
+        }
+        if (!blocking) return 0;
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_sleep(127);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
+            flag_error(P, kErrPromTimeout);
+            return -1;
+        }
+    }
+}
+
 // Tier 1 as its own kernel (the scheduled path, scenes up to kCoopLds
 // spheres): single-wave workgroups launched on the context's auxiliary
-// stream beside k_render (launch_render), each taking tier-1 slots ([0, k1)
-// of the cost-ordered queue, k_heavy_split) one at a time and tracing the
-// pixel with the whole wave (trace_pixel_uniform), at wave priority
-// prio_t1. Its own register budget (up to 128 VGPRs) keeps the wave trace's
-// state out of k_render, whose lane-mode loop it would otherwise crowd into
-// scratch. k_render skips tier 1 (KParams::trace_ext).
+// stream beside k_render (launch_render), taking tier-1 slots ([0, k1) of the
+// cost-ordered queue, k_heavy_split) and tracing each pixel with a group of
+// lanes (trace_group_segment), at wave priority prio_t1. The very heaviest
+// slots, [0, k0), go one per wave (the whole wave on one chain: the shortest
+// time per segment); the rest 2^(6 - trace_lg) per wave (trace_group: the same
+// chains for a fraction of the SIMD time). A group whose pixel ends takes the
+// next slot; once tier 1 is exhausted the idle groups serve the promotion
+// queue while k_render runs (take_promoted_groups), and a wave whose pixels
+// fill at most half its groups regroups them into larger groups (regroup:
+// shorter segments for the last chains). Its own register budget (up to 128
+// VGPRs) keeps this state out of k_render, whose lane-mode loop it would
+// otherwise crowd into scratch. k_render skips tier 1
+// (KParams::trace_ext).
 constexpr uint32_t kTraceThreads = 64;
 __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -1701,42 +1825,83 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
     const uint32_t k1 = min(P.heavy[3], min(P.heavy[1], npix));
+    const uint32_t k0 = min(P.heavy[4], k1);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lg_many = min(P.trace_lg, 6u);
     set_prio(P.prio_t1);
-    uint32_t segs = 0;
+    uint32_t lg = 6u;
+    Lane W;
+    W.active = false;
+    W.segs = 0;
+    W.seg0 = 0;
+    W.slot = 0;
+    uint32_t segs = 0;  // segments traced, counted by the first lane of each group
+    bool t1_done = k1 == 0u;
+    bool serve_done = P.prom == nullptr;
     for (;;) {
-        uint32_t slot = 0;
-        if (threadIdx.x == 0) slot = atomicAdd(P.heavy, 1u);  // the tier-1 counter
-        slot = (uint32_t)__shfl((int)slot, 0, 64);
-        if (slot >= k1) break;
-        Lane W;
-        W.segs = 0;
-        start_pixel(P, F, P.perm[slot], W);
-        diag_pixel_start(P, W.gid, 1ull);
-        trace_pixel_uniform(P, F, sl, W, nullptr, nullptr);
-        if (threadIdx.x == 0) {
-            write_pixel<false>(P, W);
-            diag_pixel_end(P, W.gid);
+        uint64_t act = __ballot(W.active);
+        if (act == 0ull && t1_done) lg = lg_many;  // an idle wave serves promotions in groups again
+        if (!t1_done) {  // idle groups take tier-1 slots, one atomic per wave
+            if (act == 0ull) {  // a wave without pixels picks its group size: solo slots one per wave
+                const uint32_t next = (uint32_t)__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(P.heavy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                lg = next < k0 ? 6u : lg_many;
+            }
+            const uint32_t g = 1u << lg;
+            const uint64_t need = __ballot(!W.active && (lane & (g - 1u)) == 0u);
+            if (need != 0ull) {
+                const uint32_t n = (uint32_t)__popcll(need);
+                uint32_t base = 0;
+                if (lane == 0u) base = atomicAdd(P.heavy, n);  // the tier-1 counter
+                base = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)base, 0, 64));
+                const uint32_t rank = (uint32_t)__popcll(need & ((1ull << (lane & ~(g - 1u))) - 1ull));
+                if (!W.active && base + rank < k1) {
+                    start_pixel(P, F, P.perm[base + rank], W);
+                    W.slot = base + rank;
+                    diag_pixel_start(P, W.gid, 1ull);
+                }
+                if (base + n >= k1) t1_done = true;
+                act = __ballot(W.active);
+            }
         }
-        segs += W.segs;
-    }
-    // then, while k_render runs, help serve the promotion queue until every
-    // pixel k_render owns (all but tier 1) is written
-    if (P.prom) {
-        Lane W;
-        W.segs = 0;
-        while (take_promoted(P, F, npix, npix - k1, true, W)) {
-            const uint32_t s0 = W.segs;
-            set_prio(P.prio_t1);
-            trace_pixel_uniform(P, F, sl, W, nullptr, nullptr);
-            if (threadIdx.x == 0) {
+        if (t1_done && !serve_done) {  // then promoted pixels, while k_render runs
+            const uint32_t g = 1u << lg;
+            const uint64_t need = __ballot(!W.active && (lane & (g - 1u)) == 0u);
+            if (need != 0ull) {
+                set_prio(P.prio_t1);
+                if (take_promoted_groups(P, F, npix, npix - k1, need, lg, act == 0ull, W) < 0) serve_done = true;
+                set_prio(P.prio_t1);
+                act = __ballot(W.active);
+            }
+        }
+        if (act == 0ull) {
+            if (t1_done && serve_done) break;
+            continue;
+        }
+        if (t1_done && lg < 6u) {  // at most half the groups busy: fewer, larger groups
+            uint32_t m = 0;
+            for (uint32_t r = 0; r < (64u >> lg); ++r) m += (uint32_t)((act >> (r << lg)) & 1ull);
+            if (2u * m <= (64u >> lg)) {
+                const uint32_t nlg = 6u - (m <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(m - 1u));
+                regroup(W, lg, nlg, act);
+                lg = nlg;
+            }
+        }
+        bool ended;
+        trace_group_segment(P, F, sl, lg, W, ended);
+        const bool first = (lane & ((1u << lg) - 1u)) == 0u;
+        if (W.active && first) segs++;
+        if (ended) {
+            if (first) {
                 write_pixel<false>(P, W);
                 diag_pixel_end(P, W.gid);
-                __hip_atomic_fetch_add(&P.prom[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (W.slot == ~0u)  // a promoted pixel: k_render's exit count
+                    __hip_atomic_fetch_add(&P.prom[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            segs += W.segs - s0;
+            W.active = false;
         }
     }
-    if (threadIdx.x == 0 && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
+    count_segments(P, segs);
 }
 
 // ---- cost-ordered pixel queue (LPT scheduling, see KSchedule) ------------
@@ -1856,6 +2021,8 @@ KTune default_tune() {
     t.prom_medium = kPromMedium;
     t.prom_large = kPromLarge;
     t.prom_big = kPromBig;
+    t.trace_group = kTraceGroup;
+    t.trace_solo = kTraceSolo;
     return t;
 }
 namespace {
@@ -1875,14 +2042,16 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     // 2- or 4-way split) also gets tier 2 above a2_medium x share
     const bool medium = !small && (double)npix < t.rho2 * (double)lanes;
     const double a2 = small ? t.a2_small : medium ? min(t.a2_medium, a1) : min(t.a2_large, a1);
-    uint32_t kh = 0, k1 = 0;
+    uint32_t kh = 0, k1 = 0, k0 = 0;
     for (uint32_t b = 0; b < kCostBuckets; ++b) {
         const double key = (double)(kCostBuckets - 1u - b);
         if (key > a2 * share) kh += counts[b];
         if (key > a1 * share) k1 += counts[b];
+        if (key > t.trace_solo * share) k0 += counts[b];  // k_trace: one pixel per wave
     }
     heavy[1] = kh;
     heavy[3] = k1;
+    heavy[4] = k0;
 }
 
 // ---- per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample) --
@@ -2367,7 +2536,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     c.perm = nullptr;  // index order
     c.heavy = nullptr;
     c.prio_slots = 0;
-    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + 8) * sizeof(uint32_t), stream);
+    e = hipMemsetAsync(sched.buckets, 0, (2 * kCostBuckets + kSchedWords) * sizeof(uint32_t), stream);
     if (e == hipSuccess) e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (pf) {
@@ -2430,7 +2599,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
                           : px_per_lane < tune.rho ? tune.prom_small : px_per_lane < tune.rho_low ? tune.prom_low
                           : px_per_lane < tune.rho2 ? tune.prom_medium : tune.prom_large;
         if (pm > 0.0 && sched.prom_q && sched.prom_cap > 0) {
-            q.prom = sched.buckets + 2 * kCostBuckets + 4;  // zeroed with the buckets
+            q.prom = sched.buckets + 2 * kCostBuckets + 8;  // zeroed with the buckets
             q.prom_q = sched.prom_q;
             q.prom_cap = sched.prom_cap;
             q.prom_min = (uint32_t)std::min<double>(pm, 4e9);
@@ -2439,6 +2608,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     }
     if (trace_waves > 0) {
         q.trace_ext = 1u;
+        q.trace_lg = 6u - (uint32_t)__builtin_ctz(max(1u, min(tune.trace_group, 64u)));
         const size_t tlds = coop_lds_bytes(p.scene.n);
         e = hipEventRecord(sched.ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(sched.aux, sched.ev_fork, 0);

@@ -796,7 +796,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_group", 0), ("trace_group", 3), ("trace_group", 32), ("trace_solo_bar", 0.0), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})
@@ -815,7 +815,9 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
                 dict(trace_small=0.0, trace_low=0.0, trace_medium=0.0, trace_large=0.0, tier1_bar=0.01,
                      tier1_bar_small=0.01, tier1_bar_low=0.01),
                 dict(trace_small=0.5, trace_low=0.5, trace_medium=0.5, trace_large=0.5, tier1_bar=0.01,
-                     tier1_bar_small=0.01, tier1_bar_low=0.01)]
+                     tier1_bar_small=0.01, tier1_bar_low=0.01),
+                dict(trace_small=0.5, trace_low=0.5, trace_medium=0.5, trace_large=0.5, tier1_bar=0.01,
+                     tier1_bar_small=0.01, tier1_bar_low=0.01, trace_group=8, trace_solo_bar=0.5)]
     for ex in extremes:
         gpu_ctx.set_schedule()
         gpu_ctx.set_schedule(**ex)
@@ -836,8 +838,10 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
     empty a lane hands its pixel to k_trace at a sample boundary (threshold 1
     projected segment: nearly every pixel still in flight is handed over,
     the 65,536-entry queue overflows on the whole frame and lanes keep the
-    rest). Whole frames and row-tile shares of every size class, against the
-    oracle bit for bit, and the frame's segment count."""
+    rest). k_trace with 1, 2, 4 and 16 pixels per wave (trace_group), the
+    heaviest alone (trace_solo_bar). Whole frames and row-tile shares of
+    every size class, against the oracle bit for bit, and the frame's
+    segment count."""
     ctx = request.getfixturevalue(ctx_name)
     world = rtx.random_world(11, depth=50, spp=12)
     W, H, T = 320, 180, 5
@@ -850,7 +854,17 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
                   dict(trace_small=0.3, trace_low=0.3, trace_medium=0.3, trace_large=0.3, promote_small=1,
                        promote_low=1, promote_medium=1, promote_large=1),
                   dict(trace_small=0.05, trace_low=0.05, trace_medium=0.05, trace_large=0.05, promote_small=50,
-                       promote_low=50, promote_medium=50, promote_large=50, tier1_bar=1.3)):
+                       promote_low=50, promote_medium=50, promote_large=50, tier1_bar=1.3),
+                  # several tier-1 pixels per k_trace wave (groups of 32 / 16 / 4 lanes), the heaviest
+                  # alone (trace_solo_bar), regrouping as tier 1 runs out, promotion served by groups
+                  dict(trace_small=0.3, trace_low=0.3, trace_medium=0.3, trace_large=0.3, tier1_bar=1.2,
+                       tier1_bar_small=1.2, tier1_bar_low=1.2, trace_group=2, trace_solo_bar=4.0),
+                  dict(trace_small=0.1, trace_low=0.1, trace_medium=0.1, trace_large=0.1, tier1_bar=0.8,
+                       tier1_bar_small=0.8, tier1_bar_low=0.8, trace_group=4, promote_small=20, promote_low=20,
+                       promote_medium=20, promote_large=20),
+                  dict(trace_small=0.05, trace_low=0.05, trace_medium=0.05, trace_large=0.05, tier1_bar=1.0,
+                       tier1_bar_small=1.0, tier1_bar_low=1.0, trace_group=16, trace_solo_bar=2.5,
+                       promote_small=1, promote_low=1, promote_medium=1, promote_large=1)):
         ctx.set_schedule()
         ctx.set_schedule(**sched)
         for nparts, part in ((1, 0), (2, 1), (4, 3), (8, 2)):

@@ -23,6 +23,7 @@ ap.add_argument("--parts", type=int, nargs="*", default=[8])
 ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--set", action="append", default=[])
+ap.add_argument("--sets", default="", help="settings separated by ';' ('default' = no change)")
 ap.add_argument("--grid", type=int, default=11, help="random_world grid half extent (159 + --max-spheres 100000: C5)")
 ap.add_argument("--max-spheres", type=int, default=0)
 ap.add_argument("--spp", type=int, default=100)
@@ -39,7 +40,8 @@ ctx = rtx.Context(0, lib=rtx.load_library(a.lib) if a.lib else None)
 ctx.upload_world(world)
 ctx.set_frame(frame)
 buf = ctx.alloc((H, W, 4))
-sets = a.set or [""]
+sets = a.set + [("" if x.strip() == "default" else x.strip()) for x in a.sets.split(";") if x.strip()]
+sets = sets or [""]
 for r in range(a.rounds):
     for s in sets:
         ctx.set_schedule()
