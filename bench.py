@@ -125,21 +125,32 @@ def pmc_traffic(args):
                          "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
 
 
-SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU",
-               "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS",
+SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU",
+               "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS",
                "GRBM_GUI_ACTIVE"]
+# where the waves' cycles go (MI355X_MICROARCH.md PMC table: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY
+# ~= WAVE_CYCLES, all in quad-cycles)
+STALL_COUNTERS = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "GRBM_GUI_ACTIVE"]
 
 
-VALU_ISSUE_MAX = 0.25  # wave64 VALU instructions per cycle per SIMD (16 lanes: 4 cycles each)
+# A wave64 fp32 VALU instruction occupies the 32-lane SIMD for 2 cycles when
+# several waves issue (one wave alone: 4) — MI355X_MICROARCH.md, cycle
+# constants: this is the issue rate behind the 157.3 TF fp32 peak (64 FLOP /
+# cycle / SIMD with v_fma_f32). Packed fp32 (v_pk_fma_f32) does twice the
+# work in twice the cycles.
+VALU_ISSUE_CYCLES = 2.0
 
 
 def pmc_valu(args, n_cu, launch_ms, rng=None):
-    """Executed-work view of the render launch (its own --pmc pass): the FP32
-    FLOPs the VALU ran, how busy the VALU issue was and how many lanes each
-    VALU instruction had. SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE
-    is summed over the 8 XCDs (MI355X_MICROARCH.md, cycle constants)."""
+    """Executed-work view of the render launch (its own --pmc passes): the FP32
+    FLOPs the VALU ran, the VALU issue rate, the lanes each VALU instruction
+    had, and where the waves' cycles went. SQ_ACTIVE_INST_* / SQ_WAVE_CYCLES
+    count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    (MI355X_MICROARCH.md, cycle constants)."""
     try:
         v = _pmc_pass(args, SQ_COUNTERS, "sq", rng)
+        w = _pmc_pass(args, STALL_COUNTERS, "stall", rng)
     except RuntimeError as e:
         return {"skipped": str(e)}
     cycles = v["GRBM_GUI_ACTIVE"] / 8.0
@@ -150,36 +161,54 @@ def pmc_valu(args, n_cu, launch_ms, rng=None):
     flops = 64.0 * (v["SQ_INSTS_VALU_FLOPS_FP32"] + v["SQ_INSTS_VALU_FLOPS_FP32_TRANS"])
     tflops = flops / (launch_ms * 1e-3) / 1e12
     ipc = v["SQ_INSTS_VALU"] / (simds * cycles)
+    wc = w["SQ_WAVE_CYCLES"]
     return {"executed_tflops": round(tflops, 3), "executed_frac": round(tflops / FP32_PEAK_TFLOPS, 4),
             "executed_tflops_active_lanes": round(tflops * lane_util, 3),
             "executed_flop_per_launch": flops,
-            "issue_frac": round(ipc / VALU_ISSUE_MAX, 4),
+            "issue_frac": round(ipc * VALU_ISSUE_CYCLES, 4),
             "valu_busy": round(4.0 * v["SQ_ACTIVE_INST_VALU"] / (simds * cycles), 4),
             "valu_lane_util": round(lane_util, 4),
             "valu_insts_per_simd_cycle": round(ipc, 4),
             "flop_per_valu_inst": round(flops / 64.0 / max(1.0, v["SQ_INSTS_VALU"]), 3),
+            "trans_share_of_valu_insts": round(v["SQ_INSTS_VALU_TRANS_F32"] / max(1.0, v["SQ_INSTS_VALU"]), 4),
+            "salu_per_valu_inst": round(v["SQ_INSTS_SALU"] / max(1.0, v["SQ_INSTS_VALU"]), 4),
+            "wave_cycles": {"resident_waves_per_simd": round(4.0 * wc / (simds * w["GRBM_GUI_ACTIVE"] / 8.0), 3),
+                            "issuing": round(w["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                            "issuing_valu": round(w["SQ_ACTIVE_INST_VALU"] / wc, 4),
+                            "issuing_salu_smem": round(w["SQ_ACTIVE_INST_SCA"] / wc, 4),
+                            "issuing_lds": round(w["SQ_ACTIVE_INST_LDS"] / wc, 4),
+                            "issuing_vmem": round(w["SQ_ACTIVE_INST_VMEM"] / wc, 4),
+                            "stalled_on_issue": round(w["SQ_WAIT_INST_ANY"] / wc, 4),
+                            "waiting_on_waitcnt": round(w["SQ_WAIT_ANY"] / wc, 4)},
             "formula": "executed = 64 * (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS) / launch time (the FP32 FLOPs "
                        "the VALU ran, prefilter, exact tests and shading included; _active_lanes scales by "
-                       "valu_lane_util); issue_frac = SQ_INSTS_VALU / (4*CUs * GRBM_GUI_ACTIVE/8 * 0.25) "
-                       "(wave64 VALU instructions issued per SIMD-cycle over their limit); "
-                       "valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8) (rocprof VALUBusy); "
-                       "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)",
-            "counters": v, "cus": n_cu}
+                       "valu_lane_util); issue_frac = 2 * SQ_INSTS_VALU / (4*CUs * GRBM_GUI_ACTIVE/8): VALU "
+                       "issue cycles at the SIMD-32's 2 cycles per wave64 instruction (the rate of the fp32 "
+                       "peak) over the SIMD-cycles; valu_busy = 4*SQ_ACTIVE_INST_VALU / (4*CUs * GRBM_GUI_ACTIVE/8) "
+                       "(rocprof VALUBusy, quad-cycle accounting: ~1 when every wave-cycle of VALU work is "
+                       "counted at 4 cycles, can read above 1 because two waves' instructions overlap); "
+                       "valu_lane_util = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU); wave_cycles: "
+                       "SQ_ACTIVE_INST_* / SQ_WAIT_INST_ANY (ready, not issued) / SQ_WAIT_ANY (s_waitcnt, "
+                       "barrier) over SQ_WAVE_CYCLES (its own pass)",
+            "counters": v, "stall_counters": w, "cus": n_cu}
 
 
 def roofline_of(executed, launch_ms, tests_per_launch):
     """The compute roofline of one launch. `frac` is the EXECUTED FP32 FLOP
     rate over the FP32 peak (PMC counters over the live launch time: <= 1 by
-    construction); `issue_frac` is the VALU-issue fraction, the roof that
-    binds this kernel (its instructions are mostly not full-rate FMAs, so it
-    saturates issue at under half the FLOP peak). The reference-algorithm
-    rate — 20 FLOP for every ray-sphere test of every segment — is reported
+    construction); `issue_frac` is the VALU issue cycles (2 per wave64
+    instruction on the 32-lane SIMD, the rate of that peak) over the
+    SIMD-cycles (<= 1 by construction); `executed.wave_cycles` says where the
+    waves' cycles go (issuing, ready but not issued, waiting on s_waitcnt).
+    The reference-algorithm rate — 20 FLOP for every ray-sphere test of
+    every segment — is reported
     as `effective_tflops`: an effective-work rate, not a roofline fraction
     (the prefilter executes 5-7 FLOP per test plus exact tests of the few
     flagged spheres, so it can exceed what the ALUs run)."""
     eff = FLOP_PER_TEST * tests_per_launch / (launch_ms * 1e-3) / 1e12
-    r = {"bound": "fp32-valu", "binding": "VALU issue (issue_frac)",
-         "roof": "fp32 vector ALU, 157.3 TF; VALU issue 0.25 wave-instructions/cycle/SIMD (the kernel issues no MFMA)",
+    r = {"bound": "fp32-valu",
+         "roof": "fp32 vector ALU, 157.3 TF = 1,024 SIMD-32s x 64 FLOP/cycle x 2.4 GHz, i.e. one wave64 v_fma_f32 "
+                 "per SIMD every 2 cycles (the kernel issues no MFMA)",
          "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None,
          "frac_kind": "executed FP32 FLOP/s / FP32 peak",
          "issue_frac": None}
