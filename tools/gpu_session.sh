@@ -32,7 +32,7 @@ for s in $STEPS; do
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                 python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
     c3b)    run c3b 900 python bench.py --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 ;;
-    c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 ;;
+    c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --per-sample ${C5PS:-0} ;;
     c3ps)   run c3ps 900 python bench.py --rng per-sample --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 ;;
     c5ps)   run c5ps 900 python bench.py --rng per-sample --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 ;;
     variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ${VARGS:-} ${VNAMES:-} ;;

@@ -3,4 +3,4 @@
 export VNAMES="promR promE" VROUNDS=4
 export HPARTS="8 4" HROUNDS=2
 export HSETS='--sets default;tg=2;tg=4;tg=2,a1s=2.0,a1l=2.4;tg=4,a1s=1.6,a1l=2.0;tg=2,prs=300,prl=400;tg=4,prs=200,prl=300;tg=4,a1s=1.6,a1l=2.0,prs=200,prl=300;tg=2,tsolo=6;tg=4,tsolo=6,a1s=1.6,a1l=2.0'
-bash tools/gpu_session.sh R6b tests variants hsweep bench
+bash tools/gpu_session.sh R6b tests variants hsweep bench c5b
