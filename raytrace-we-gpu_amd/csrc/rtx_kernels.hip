@@ -277,7 +277,27 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 #ifndef RTX_PF_LDS  // large scenes stream through a per-wave LDS tile of RTX_PF_LDS KiB (below; 0: SGPR double buffer)
 #define RTX_PF_LDS 1  // C5 1,880-1,907 -> 1,811-1,847 ms (profiles/R3w_*, R3x_*)
 #endif
-constexpr uint32_t kPfLdsBytes = (kRB / 64) * 64 * 16 * RTX_PF_LDS;  // RTX_PF_LDS KiB per wave
+#ifndef RTX_PF_RING  // A/B: the tile stream as a ring of RTX_PF_RING 1-KiB slots filled by LDS-DMA (0: VGPR staging)
+#define RTX_PF_RING 0
+#endif
+constexpr uint32_t kPfSlots = RTX_PF_RING > RTX_PF_LDS ? RTX_PF_RING : RTX_PF_LDS;
+constexpr uint32_t kPfLdsBytes = (kRB / 64) * 64 * 16 * kPfSlots;  // kPfSlots KiB per wave
+// LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes at gsrc land at LDS byte
+// address lds_base + 16 l (wave-uniform base, in M0). An asm load is outside
+// the compiler's s_waitcnt bookkeeping: the caller counts it with vmcnt. The
+// lgkmcnt(0) first: the slot's earlier ds_reads have returned before it is
+// overwritten.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base) {
+    unsigned keep;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_base)
+                 : "memory");
+}
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
 #define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
 #endif
@@ -332,7 +352,53 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
         return false;
     };
     full = true;
-    if (kPF && RTX_PF_LDS && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
+    if (kPF && RTX_PF_RING && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
+        // A/B build: the scene streams through a ring of
+        // kNR 1-KiB slots (8 blocks each) per wave, filled by LDS-DMA with no
+        // VGPR staging: kNR - 1 tiles in flight while one is scanned. Before
+        // tile j is scanned, tile j + kNR - 1 is issued into the slot tile
+        // j - 1 used, and vmcnt(kNR - 1) retires tile j (vector-memory
+        // operations complete in issue order). Tiles past `end` re-read the
+        // last block (a constant count of loads in flight); a scan that stops
+        // for a full list leaves its loads in flight (the next scan's counted
+        // waits cover them: they are older), one that reaches `end` drains.
+        // Every lane of the wave runs this (the DMA writes one 16-byte piece
+        // per lane).
+        constexpr uint32_t kNR = RTX_PF_RING ? RTX_PF_RING : 2u;  // (the branch is dead when 0)
+        static_assert(kNR >= 2 && kNR <= 8, "ring of 2..8 slots");
+        float4 *ring = const_cast<float4 *>(reinterpret_cast<const float4 *>(lds_pr)) +
+                       64u * kNR * ((threadIdx.x & 255u) >> 6);
+        const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(ring));
+        const float4 *gp = (const float4 *)(const float *)pre;
+        const uint32_t lane = threadIdx.x & 63u;
+        auto issue = [&](uint32_t tb, uint32_t slot) {
+            glds16(gp + 8u * min(tb + (lane >> 3), end - 1u) + (lane & 7u), rbase + 1024u * slot);
+        };
+        uint32_t tb = b - b % 8u;
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < kNR; ++k) issue(tb + 8u * k, k);
+        for (uint32_t j = 0;; ++j) {
+            issue(tb + 8u * (kNR - 1u), (j + kNR - 1u) % kNR);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNR - 1u) : "memory");
+            const float4 *q0 = ring + 64u * (j % kNR);
+            const uint32_t e = min(tb + 8u, end);
+            for (; b < e; ++b) {
+                const float4 *q = q0 + 8u * (b - tb);
+                float4 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = q[t];
+                auto blk = [&](int i) {
+                    const float4 w = v[i >> 2];
+                    const int c = i & 3;
+                    return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
+                };
+                if (step(blk, b)) return b + 1;
+            }
+            if (tb + 8u >= end) break;
+            tb += 8u;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (kPF && RTX_PF_LDS && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
         // A/B build: the scene streams through a per-wave
         // LDS tile of 8 * RTX_PF_LDS blocks (RTX_PF_LDS KiB: coalesced 16-byte
         // loads, one per lane per KiB, the next tile's loads in flight while
@@ -1597,7 +1663,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
-    const float *pf_tile = kPF && RTX_PF_LDS ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
+    const float *pf_tile = kPF && (RTX_PF_LDS || RTX_PF_RING) ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
     // promotion: the block's first wave to go idle serves the queue, the others leave
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
@@ -1694,7 +1760,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // so its time per segment is not stretched by the SIMD's other waves
         set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
         bool promoted = false;
-        if (RTX_PF_LDS && kPF) {  // A/B build: every lane of the wave fills the scan's LDS tile
+        if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
             float best = __uint_as_float(0x7f800000u);
             const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
