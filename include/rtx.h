@@ -40,8 +40,9 @@ extern "C" {
 
 #define RTX_VERSION 130 /* 1.3.0 */
 /* ABI notes.
- *  1.3.0: rtx_schedule.trace_solo_bar (after promote_big_scene) and
- *         trace_group (after refill_chunk): the struct grew by 8 bytes;
+ *  1.3.0: rtx_schedule.trace_solo_bar (after promote_big_scene),
+ *         trace_group and prepass_cap_split (after refill_chunk): the
+ *         struct grew by 12 bytes;
  *         rtx_build_info; RTX_ERR_INCOMPLETE: rtx_sync, rtx_download, rtx_get_stats and
  *         rtx_stats_reset report a render launch that left pixels unwritten
  *         (the promotion service's safety valve fired) instead of returning
@@ -245,6 +246,9 @@ typedef struct rtx_schedule {
     uint32_t hot_priority;    /* default 3 */
     uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
     uint32_t trace_group;     /* default 1: tier-1 pixels per wave of the tier-1 kernel (1, 2, 4, 8, 16) */
+    uint32_t prepass_cap_split; /* default 0 (none): a row-split part's cost pre-pass stops a pixel past this
+                                   many segments (0..4096); it goes to the top of the queue (tier 1) and the
+                                   render traces it from sample 0 */
     uint32_t reserved;        /* must be 0 */
 } rtx_schedule;
 /* The library's defaults (no context, no GPU). */
@@ -254,7 +258,7 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
  * tail_coop_max and tail_coop_max_large in 1..64,
  * priorities in 0..3, refill_chunk in 0..4096, trace_group a power of two
- * in 1..16, trace_solo_bar > 0, reserved 0. */
+ * in 1..16, trace_solo_bar > 0, prepass_cap_split in 0..4096, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 

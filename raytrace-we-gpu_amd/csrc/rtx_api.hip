@@ -297,6 +297,7 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->refill_chunk = t.chunk;
     out->trace_group = t.trace_group;
     out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
+    out->prepass_cap_split = t.cap_split;
     return RTX_OK;
 }
 
@@ -335,6 +336,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     if (s->refill_chunk > 4096) return fail(RTX_ERR_INVALID, "rtx_set_schedule: refill_chunk must be in 0..4096");
     if (s->trace_group < 1 || s->trace_group > 16 || (s->trace_group & (s->trace_group - 1)) != 0)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_group must be 1, 2, 4, 8 or 16");
+    if (s->prepass_cap_split > 4096)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: prepass_cap_split must be in 0..4096");
     if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
     rtx::KTune t;
     t.a1 = s->tier1_bar;
@@ -367,6 +370,7 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.chunk = s->refill_chunk;
     t.trace_group = s->trace_group;
     t.trace_solo = s->trace_solo_bar;
+    t.cap_split = s->prepass_cap_split;
     c->tune = t;
     return RTX_OK;
 }
@@ -405,6 +409,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->refill_chunk = t.chunk;
     out->trace_group = t.trace_group;
     out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
+    out->prepass_cap_split = t.cap_split;
     return RTX_OK;
 }
 

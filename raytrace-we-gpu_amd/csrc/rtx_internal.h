@@ -112,6 +112,7 @@ struct KTune {
     double prom_big;                                           // ... for scenes without the coop's LDS copy
     uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2, 4, 8)
     double trace_solo;                                         // ... one per wave above this x share (k0)
+    uint32_t cap_split;                                        // pre-pass cap of a row-split part (0: none)
 };
 KTune default_tune();
 

@@ -117,6 +117,8 @@ constexpr double kPromBig = 60.0;
 // above which a pixel is traced alone in its wave nonetheless
 constexpr uint32_t kTraceGroup = 1;
 constexpr double kTraceSolo = 1e30;
+// pre-pass segment cap for row-split parts (0: none; see launch_render)
+constexpr uint32_t kCapSplit = 0;
 // Cost pre-pass cap (whole-frame parts only: in a row-split share a capped,
 // under-rated key keeps heavy pixels out of the tiers — parts 2/4/8 30/21/15
 // -> 34/26/26 ms, profiles/R4h_parts.jsonl): a pixel still tracing after
@@ -1975,15 +1977,23 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
 // key is the sum over a (2R+1)^2 window of neighbouring pixels (clamped
 // at the edges), which averages that noise over similar pixels.
 constexpr int kLptRadius = 1;  // 3x3 window (radius 0 was 36 % slower, radius 2 5 % slower)
+// sat_cap (row-split parts with a pre-pass cap, KTune::cap_split): a pixel
+// the pre-pass stopped (cost kCostSaturated) takes the top bucket itself,
+// and counts as sat_cap segments in its neighbours' windows (0: a stopped
+// pixel's saturated cost saturates every window it is in, as for large
+// scenes).
+constexpr uint32_t kCostSaturated = 0xffffu;
 __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, uint32_t width, uint32_t rows,
-                                             uint32_t cost_spp) {
+                                             uint32_t cost_spp, uint32_t sat_cap) {
+    if (sat_cap != 0u && cost[i] == kCostSaturated) return 0u;  // bucket 0 = most expensive
     const int x = (int)(i % width), y = (int)(i / width);
     uint32_t sum = 0;
     for (int dy = -kLptRadius; dy <= kLptRadius; ++dy) {
         const int yy = min(max(y + dy, 0), (int)rows - 1);
         for (int dx = -kLptRadius; dx <= kLptRadius; ++dx) {
             const int xx = min(max(x + dx, 0), (int)width - 1);
-            sum += cost[(uint32_t)yy * width + (uint32_t)xx];
+            const uint32_t c = cost[(uint32_t)yy * width + (uint32_t)xx];
+            sum += (sat_cap != 0u && c == kCostSaturated) ? sat_cap : c;
         }
     }
     // scaled to 9 one-sample costs (the 3x3, 1-spp key the tiers were tuned on)
@@ -1994,7 +2004,7 @@ __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, u
 constexpr uint32_t kSortPerThread = 16;
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
-                                                      uint32_t cost_spp, uint32_t *counts) {
+                                                      uint32_t cost_spp, uint32_t sat_cap, uint32_t *counts) {
     __shared__ uint32_t h[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -2002,7 +2012,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp)], 1u);
+        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
@@ -2014,7 +2024,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // order within a bucket is arbitrary; per-pixel results do not depend on it.
 // (Tile-major order within a bucket measured no faster: DESIGN.md §7.)
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
-                                                         uint32_t cost_spp,
+                                                         uint32_t cost_spp, uint32_t sat_cap,
                                                          const uint32_t *counts, uint32_t *cursors,
                                                          uint32_t *perm) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
@@ -2025,7 +2035,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        key[k] = i < n ? cost_key(cost, i, width, rows, cost_spp) : 0u;
+        key[k] = i < n ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
         rank[k] = i < n ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
     __syncthreads();
@@ -2089,6 +2099,7 @@ KTune default_tune() {
     t.prom_big = kPromBig;
     t.trace_group = kTraceGroup;
     t.trace_solo = kTraceSolo;
+    t.cap_split = kCapSplit;
     return t;
 }
 namespace {
@@ -2588,11 +2599,15 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // large scenes: one sample — there a segment costs ~4 ms of wave time and
     // the pre-pass waits on its heaviest pixel's chain
     c.spp = min(p.spp, pf ? kCostSppLarge : kCostSpp);
+    uint32_t split_cap = 0;
     {
         const uint32_t rb = resident_blocks(render_fn<true, false>(pf), lds);
         const bool whole = (double)lanes >= tune.rho2 * (double)min(need, rb) * kRB;  // a large part (the tiers' class)
-        c.cost_cap = whole ? (pf ? kCostCapLarge : kCostCap) : 0u;
-        c.cost_capped = pf ? 0xffffu : c.cost_cap;
+        // a row-split share (small scenes) may cap too (cap_split): its stopped
+        // pixels take the top bucket (tier 1), their neighbours count the cap
+        split_cap = !whole && !pf ? min(tune.cap_split, 4096u) : 0u;
+        c.cost_cap = whole ? (pf ? kCostCapLarge : kCostCap) : split_cap;
+        c.cost_capped = (pf || split_cap != 0u) ? kCostSaturated : c.cost_cap;
     }
     c.chunk = 0;  // (private runs for the large-scene pre-pass: no faster)
     c.cost_out = sched.cost;
@@ -2617,7 +2632,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // 2. counting sort by cost, descending
     const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, sched.buckets);
+                       p.rows_local, c.spp, split_cap, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
     uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
@@ -2630,7 +2645,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy,
                        tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
+                       p.rows_local, c.spp, split_cap, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
     KParams q = p;
     q.cost_spp = c.spp;
     q.perm = sched.perm;

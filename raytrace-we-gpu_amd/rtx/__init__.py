@@ -67,7 +67,7 @@ class rtx_schedule(C.Structure):
                 ("trace_solo_bar", C.c_float),
                 ("tail_coop_max", C.c_uint32), ("tail_coop_max_large", C.c_uint32), ("tier1_priority", C.c_uint32), ("tier2_priority", C.c_uint32),
                 ("hot_priority", C.c_uint32), ("refill_chunk", C.c_uint32), ("trace_group", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("prepass_cap_split", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}

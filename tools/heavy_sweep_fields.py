@@ -7,7 +7,8 @@ SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a
          "coop": "tail_coop_max", "coopL": "tail_coop_max_large", "p1": "tier1_priority", "trs": "trace_small", "trl": "trace_low",
          "trm": "trace_medium", "trL": "trace_large", "prs": "promote_small", "prl": "promote_low",
          "prm": "promote_medium", "prL": "promote_large", "prB": "promote_big_scene", "p2": "tier2_priority", "ph": "hot_priority",
-         "chunk": "refill_chunk", "tg": "trace_group", "tsolo": "trace_solo_bar"}
+         "chunk": "refill_chunk", "tg": "trace_group", "tsolo": "trace_solo_bar",
+         "capS": "prepass_cap_split"}
 
 
 def schedule_of(setting):
@@ -15,5 +16,5 @@ def schedule_of(setting):
     for kv in filter(None, setting.split(",")):
         k, v = kv.split("=")
         k = SHORT.get(k.strip(), k.strip())
-        fields[k] = int(v) if k.startswith("tail_coop_max") or k.endswith("priority") or k in ("refill_chunk", "trace_group") else float(v)
+        fields[k] = int(v) if k.startswith("tail_coop_max") or k.endswith("priority") or k in ("refill_chunk", "trace_group", "prepass_cap_split") else float(v)
     return fields
