@@ -1504,12 +1504,22 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? lo : 0u, lg);
     const uint64_t win = __ballot(ib != 0u && lo == ib && cb0 == cb) & gm;  // lanes holding the group's winner
     const uint64_t bad = __ballot(!ok) & gm;                               // a non-finite root in the group
-    // the winner's material from its lane (every lane takes part in the permutes)
-    const int wl = win != 0ull ? (int)__builtin_ctzll(win) : (int)lane;
+    // the winner's material from its lane: v_readlane when the group is the
+    // whole wave (lg 6: uniform), else a permute (every lane takes part)
     HitMat M;
-    M.mt = __shfl(mt_l, wl, 64);
-    M.mv = make_float4(__shfl(mv_l.x, wl, 64), __shfl(mv_l.y, wl, 64), __shfl(mv_l.z, wl, 64),
-                       __shfl(mv_l.w, wl, 64));
+    if (lg >= 6u) {
+        const int wl = win != 0ull ? (int)__builtin_ctzll(win) : 0;
+        M.mt = __builtin_amdgcn_readlane(mt_l, wl);
+        M.mv = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.x), wl)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.y), wl)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.z), wl)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.w), wl)));
+    } else {
+        const int wl = win != 0ull ? (int)__builtin_ctzll(win) : (int)lane;
+        M.mt = __shfl(mt_l, wl, 64);
+        M.mv = make_float4(__shfl(mv_l.x, wl, 64), __shfl(mv_l.y, wl, 64), __shfl(mv_l.z, wl, 64),
+                           __shfl(mv_l.w, wl, 64));
+    }
     ended = false;
     if (!W.active) return;
     int hit = -1;
