@@ -936,6 +936,15 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
     return active ? result : -1;
 }
 
+#ifndef RTX_AB_NOP3  // A/B switches (round-4 bisection of the C2 loss; 0 = product)
+#define RTX_AB_NOP3 0
+#endif
+#ifndef RTX_AB_NOFLAG
+#define RTX_AB_NOFLAG 0
+#endif
+#ifndef RTX_AB_OLDTP
+#define RTX_AB_OLDTP 0
+#endif
 #ifndef RTX_PROM_EXACT_RATE  // A/B: a restarted pixel's promotion rate over its samples from 0 (1) or from cost_spp (0)
 #define RTX_PROM_EXACT_RATE 1
 #endif
@@ -1305,7 +1314,7 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
         L.seed = pixel_seed(P, L.x, L.y, 0);
-        if (P.state && !P.cost_out) L.seg0 |= kSeg0Restart;  // promote() counts its samples from 0
+        if (!RTX_AB_NOFLAG && P.state && !P.cost_out) L.seg0 |= kSeg0Restart;  // promote() counts its samples from 0
     }
     L.active = true;
     begin_sample(P, F, L.x, L.y, L);
@@ -1609,7 +1618,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         const uint32_t done = ld(&P.prom[2]);
         if (done >= target) return false;
         if (helper && ld(&P.prom[3]) == 0u) return false;  // k_render has not started: it serves itself
-        if (done != seen) {  // progress: the valve restarts
+        if (!RTX_AB_OLDTP && done != seen) {  // progress: the valve restarts
             seen = done;
             t0 = __builtin_amdgcn_s_memrealtime();
         }
@@ -1682,7 +1691,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     if (kPF && threadIdx.x == 0) *pack = 0u;
     if (prom_on && threadIdx.x == 0) {
         s_server = 0u;
-        __hip_atomic_fetch_add(&P.prom[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_render runs
+        if (!RTX_AB_NOP3) __hip_atomic_fetch_add(&P.prom[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_render runs
     }
     if (coop_lds || kPF || prom_on) __syncthreads();
     const int last = (int)P.scene.n - 1;
