@@ -79,7 +79,7 @@ struct KParams {
     // wave hands a pixel whose projected remaining segments exceed prom_min
     // to k_trace at a sample boundary (rtx_kernels.hip, promote)
     uint32_t *prom;                // [0] entries claimed [1] entries taken [2] k_render-owned pixels written
-                                   // [3] k_render workgroups started; NULL: off
+                                   // [3] k_render has started (set by its workgroup 0); NULL: off
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;

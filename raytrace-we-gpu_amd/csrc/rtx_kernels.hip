@@ -936,15 +936,6 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
     return active ? result : -1;
 }
 
-#ifndef RTX_AB_NOP3  // A/B switches (round-4 bisection of the C2 loss; 0 = product)
-#define RTX_AB_NOP3 0
-#endif
-#ifndef RTX_AB_NOFLAG
-#define RTX_AB_NOFLAG 0
-#endif
-#ifndef RTX_AB_OLDTP
-#define RTX_AB_OLDTP 0
-#endif
 #ifndef RTX_PROM_EXACT_RATE  // A/B: a restarted pixel's promotion rate over its samples from 0 (1) or from cost_spp (0)
 #define RTX_PROM_EXACT_RATE 1
 #endif
@@ -1314,7 +1305,7 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
         L.seed = pixel_seed(P, L.x, L.y, 0);
-        if (!RTX_AB_NOFLAG && P.state && !P.cost_out) L.seg0 |= kSeg0Restart;  // promote() counts its samples from 0
+        if (P.state && !P.cost_out) L.seg0 |= kSeg0Restart;  // promote() counts its samples from 0
     }
     L.active = true;
     begin_sample(P, F, L.x, L.y, L);
@@ -1595,9 +1586,10 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
 // them, so the count reaches `target` only when the queue holds nothing
 // more. The tail is read after the count: a pixel is promoted (slot claimed,
 // entry stored) before its old wave can go idle and flush. `helper` (k_trace):
-// serve only while k_render runs — prom[3] counts its started workgroups; a
-// k_trace that sees none leaves (k_render then serves its own promotions),
-// one that sees some waits on a kernel that is already running. All relaxed
+// serve only while k_render runs — prom[3] is set by its first workgroup; a
+// k_trace that sees it unset leaves (k_render then serves its own
+// promotions), one that sees it set waits on a kernel that is already
+// running. All relaxed
 // (agent_store_order). Polls sleep ~8k clocks at priority 0. Safety valve: a
 // server that sees no pixel written for kPromValveTicks leaves and flags the
 // launch (KParams::errors: rtx_sync / rtx_get_stats report it), so a bug shows
@@ -1618,7 +1610,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         const uint32_t done = ld(&P.prom[2]);
         if (done >= target) return false;
         if (helper && ld(&P.prom[3]) == 0u) return false;  // k_render has not started: it serves itself
-        if (!RTX_AB_OLDTP && done != seen) {  // progress: the valve restarts
+        if (done != seen) {  // progress: the valve restarts
             seen = done;
             t0 = __builtin_amdgcn_s_memrealtime();
         }
@@ -1689,10 +1681,13 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
     if (kPF && threadIdx.x == 0) *pack = 0u;
-    if (prom_on && threadIdx.x == 0) {
-        s_server = 0u;
-        if (!RTX_AB_NOP3) __hip_atomic_fetch_add(&P.prom[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_render runs
-    }
+    if (prom_on && threadIdx.x == 0) s_server = 0u;
+    // "k_render runs" for k_trace's promotion service (take_promoted): one
+    // plain store by one workgroup. A returning atomic by every workgroup
+    // here, waited for at the barrier below, cost the C2 frame 4-7 ms
+    // (43.7 vs 47.9-51 ms, profiles/R6d_ab_c2_bisect.jsonl).
+    if (prom_on && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&P.prom[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (coop_lds || kPF || prom_on) __syncthreads();
     const int last = (int)P.scene.n - 1;
     const Frame F = load_frame(P);
