@@ -1442,9 +1442,15 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // One segment of every active group (the group's lanes hold its pixel's
 // state W; lanes of groups without a pixel flag nothing); `ended`: the
 // group's pixel finished its last sample (W.acc, W.seed final).
-template <typename Src>
-__device__ __forceinline__ void trace_group_segment(const KParams &P, const Frame &F, const Src &src, uint32_t lg,
-                                                    Lane &W, bool &ended) {
+// kLg: the group size is a compile-time constant (k_trace dispatches on the
+// wave's lg): the shifts, the reduction's DPP steps and the winner's
+// material fetch are then as cheap as in a whole-wave-only kernel (a
+// runtime lg cost the one-pixel-per-wave case 2.0 -> 2.5 us per segment,
+// profiles/R6f_pixel_timeline_r8.jsonl).
+template <uint32_t kLg, typename Src>
+__device__ __forceinline__ void trace_group_segment(const KParams &P, const Frame &F, const Src &src, Lane &W,
+                                                    bool &ended) {
+    constexpr uint32_t lg = kLg;
     const KScene &S = P.scene;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t g = 1u << lg, k = lane & (g - 1u);
@@ -1507,7 +1513,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     // the winner's material from its lane: v_readlane when the group is the
     // whole wave (lg 6: uniform), else a permute (every lane takes part)
     HitMat M;
-    if (lg >= 6u) {
+    if constexpr (lg >= 6u) {
         const int wl = win != 0ull ? (int)__builtin_ctzll(win) : 0;
         M.mt = __builtin_amdgcn_readlane(mt_l, wl);
         M.mv = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mv_l.x), wl)),
@@ -1909,7 +1915,7 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     const uint32_t k1 = min(P.heavy[3], min(P.heavy[1], npix));
     const uint32_t k0 = min(P.heavy[4], k1);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lg_many = min(P.trace_lg, 6u);
+    const uint32_t lg_many = min(max(P.trace_lg, 4u), 6u);
     set_prio(P.prio_t1);
     uint32_t lg = 6u;
     Lane W;
@@ -1970,7 +1976,11 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             }
         }
         bool ended;
-        trace_group_segment(P, F, sl, lg, W, ended);
+        switch (lg) {  // wave-uniform; trace_group 1, 2, 4 (rtx_set_schedule)
+            case 6: trace_group_segment<6>(P, F, sl, W, ended); break;
+            case 5: trace_group_segment<5>(P, F, sl, W, ended); break;
+            default: trace_group_segment<4>(P, F, sl, W, ended); break;
+        }
         const bool first = (lane & ((1u << lg) - 1u)) == 0u;
         if (W.active && first) segs++;
         if (ended) {
