@@ -1459,7 +1459,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const int last = (int)S.n - 1;
     const ScatterSpec sp = scatter_spec(W.seed);
     LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
-    if (!W.active) {  // no pixel: nothing is flagged
+    if (lg < 6u && !W.active) {  // a group without a pixel: nothing is flagged (a whole wave is always active)
         T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
         T.thr = inf;
     }
@@ -1527,7 +1527,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
                            __shfl(mv_l.w, wl, 64));
     }
     ended = false;
-    if (!W.active) return;
+    if (lg < 6u && !W.active) return;
     int hit = -1;
     float t = inf;
     if (bad != 0ull) {  // the exact in-order scan, the group's ray in every lane of it
@@ -1976,13 +1976,24 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             }
         }
         bool ended;
-        switch (lg) {  // wave-uniform; trace_group 1, 2, 4 (rtx_set_schedule)
-            case 6: trace_group_segment<6>(P, F, sl, W, ended); break;
-            case 5: trace_group_segment<5>(P, F, sl, W, ended); break;
-            default: trace_group_segment<4>(P, F, sl, W, ended); break;
-        }
         const bool first = (lane & ((1u << lg) - 1u)) == 0u;
-        if (W.active && first) segs++;
+        if (lg == 6u) {
+            // one pixel in the whole wave: trace it to its end in a tight loop
+            // (no group bookkeeping between segments: the per-segment latency
+            // is this pixel's critical path)
+            uint32_t n = 0;
+            do {
+                trace_group_segment<6>(P, F, sl, W, ended);
+                ++n;
+            } while (!ended);
+            if (first) segs += n;
+        } else {
+            if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 (rtx_set_schedule)
+                trace_group_segment<5>(P, F, sl, W, ended);
+            else
+                trace_group_segment<4>(P, F, sl, W, ended);
+            if (W.active && first) segs++;
+        }
         if (ended) {
             if (first) {
                 write_pixel<false>(P, W);
