@@ -216,8 +216,8 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  * measured best. A context starts with the defaults. */
 typedef struct rtx_schedule {
     float tier1_bar;          /* default 1.7 */
-    float tier1_bar_small;    /* default 2.5 */
-    float tier1_bar_low;      /* default 3.0 */
+    float tier1_bar_small;    /* default 1.6 */
+    float tier1_bar_low;      /* default 2.0 */
     float tier2_bar_small;    /* default 2.0 */
     float tier2_bar_medium;   /* default 1.2 */
     float tier2_bar;          /* default 1e30 (no tier 2 for a larger part) */
@@ -228,24 +228,24 @@ typedef struct rtx_schedule {
     float occupancy_small;    /* default 1.0; each occupancy in (0, 1] */
     float occupancy_low;      /* default 1.0 */
     float occupancy_normal;   /* default 1.0 */
-    float trace_small;        /* default 0.25; each trace_* in [0, 0.5] */
-    float trace_low;          /* default 0.2 */
-    float trace_medium;       /* default 0 */
+    float trace_small;        /* default 0.35; each trace_* in [0, 0.5] */
+    float trace_low;          /* default 0.3 */
+    float trace_medium;       /* default 0.15 */
     float trace_large;        /* default 0 */
-    float promote_small;      /* default 0; each promote_* in [0, 1e9] */
-    float promote_low;        /* default 0 */
-    float promote_medium;     /* default 500 */
+    float promote_small;      /* default 400; each promote_* in [0, 1e9] */
+    float promote_low;        /* default 300 */
+    float promote_medium;     /* default 400 */
     float promote_large;      /* default 400 */
     float promote_big_scene;  /* default 60: every part of a scene above 640 spheres */
-    float trace_solo_bar;     /* default 1e30 (none): tier-1 keys above this x share are traced one pixel
-                                 per wave even when trace_group > 1 */
+    float trace_solo_bar;     /* default 6: tier-1 keys above this x share are traced one pixel per wave
+                                 even when trace_group > 1 */
     uint32_t tail_coop_max;   /* default 32 */
     uint32_t tail_coop_max_large; /* default 8: the same for scenes above 640 spheres */
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
     uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
-    uint32_t trace_group;     /* default 1: tier-1 pixels per wave of the tier-1 kernel (1, 2 or 4) */
+    uint32_t trace_group;     /* default 4: tier-1 pixels per wave of the tier-1 kernel (1, 2 or 4) */
     uint32_t prepass_cap_split; /* default 0 (none): a row-split part's cost pre-pass stops a pixel past this
                                    many segments (0..4096); it goes to the top of the queue (tier 1) and the
                                    render traces it from sample 0 */

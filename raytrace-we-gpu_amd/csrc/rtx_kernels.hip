@@ -92,31 +92,31 @@ constexpr uint32_t kHeavy2 = 8;         // tier-2 heavy pixels per group-coop wa
 constexpr uint32_t kHeavy1 = 1;         // tier-1 heavy pixels per wave
 constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha * a lane's share of the summed keys
 constexpr double kHeavy1Alpha = 1.7;    // tier 1 iff key > alpha1 * share
-constexpr double kHeavy1AlphaSmall = 2.5;   // the same for a small frame share (4.0 until R4b: with k_trace)
+constexpr double kHeavy1AlphaSmall = 1.6;   // the same for a small frame share (2.5 until round 4, 4.0 until R4b)
 constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than this * resident lanes
-constexpr double kHeavy1AlphaLow = 3.0;     // tier-1 bar for a low share (3.5 until R4b)
+constexpr double kHeavy1AlphaLow = 2.0;     // tier-1 bar for a low share (3.0 until round 4, 3.5 until R4b)
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > this * share (2-way split: 37 -> 34 ms, r5a-b)
 constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (default: none)
 // k_trace waves (tier 1 outside k_render) as a fraction of the resident waves, by share class.
-// With the tier-1 bars above: parts 8 15.75 -> 15.20 ms, parts 4 21.14 -> 20.57 ms (medians of 4,
-// profiles/R4b_sweep_r4_r8_trace.jsonl; R3r/R3u swept the fractions and bars). Medium shares and the whole frame
-// are no faster with it (R3h: 30.7 vs 44 ms with 5 % at R = 2: its few waves queue the many
-// medium-share tier-1 pixels).
-constexpr double kTraceSmall = 0.25, kTraceLow = 0.2, kTraceMedium = 0.0, kTraceLarge = 0.0;
+// Round 4 (k_trace traces 4 tier-1 pixels per wave, the heaviest alone; profiles/R6i_*, R6j_*): with
+// the tier-1 bars above and promotion for small / low / medium shares, parts 8 15.0 -> 13.2-13.8 ms,
+// parts 4 20.3 -> 19.6-20.0, parts 2 29.6 -> 28.5. The whole frame is no faster with it.
+constexpr double kTraceSmall = 0.35, kTraceLow = 0.3, kTraceMedium = 0.15, kTraceLarge = 0.0;
 // promotion thresholds (projected further segments; 0: off): a whole frame
 // 50.0 -> 46.5 ms at 300-500 (700: 48.5, 1000: 49-51); a 2-way split
-// 30.6-31.1 -> 29.6-30.0 ms at 250-500; 4- and 8-way splits 1-2 ms slower
-// at any threshold
-constexpr double kPromSmall = 0.0, kPromLow = 0.0, kPromMedium = 500.0, kPromLarge = 400.0;
+// 30.6-31.1 -> 29.6-30.0 ms at 250-500; 4- and 8-way splits: with k_trace's
+// pixel groups serving the queue, 300-400 (150: 40 ms at R = 8, the queue
+// floods; profiles/R6j_*)
+constexpr double kPromSmall = 400.0, kPromLow = 300.0, kPromMedium = 400.0, kPromLarge = 400.0;
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
 // k_trace: tier-1 pixels per wave (1, 2, 4, 8), and the key bar (x share)
 // above which a pixel is traced alone in its wave nonetheless
-constexpr uint32_t kTraceGroup = 1;
-constexpr double kTraceSolo = 1e30;
+constexpr uint32_t kTraceGroup = 4;
+constexpr double kTraceSolo = 6.0;
 // pre-pass segment cap for row-split parts (0: none; see launch_render)
 constexpr uint32_t kCapSplit = 0;
 // Cost pre-pass cap (whole-frame parts only: in a row-split share a capped,

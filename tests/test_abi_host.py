@@ -103,17 +103,18 @@ def test_schedule_defaults_and_validation(rtx):
     defaults are the measured constants, and rtx_set_schedule validates every
     field before a context exists (a null ctx is refused first)."""
     d = rtx.schedule_defaults()
-    assert d.tier1_bar == pytest.approx(1.7) and d.tier1_bar_small == pytest.approx(2.5)
-    assert d.tier1_bar_low == pytest.approx(3.0) and d.tier2_bar_small == pytest.approx(2.0)
+    assert d.tier1_bar == pytest.approx(1.7) and d.tier1_bar_small == pytest.approx(1.6)
+    assert d.tier1_bar_low == pytest.approx(2.0) and d.tier2_bar_small == pytest.approx(2.0)
     assert d.tier2_bar_medium == pytest.approx(1.2) and d.small_share == pytest.approx(1.2)
     assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
     assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 32 and d.tail_coop_max_large == 8
     assert d.refill_chunk == 16
     assert d.tier2_bar == pytest.approx(1e30)
     assert (d.tier1_priority, d.tier2_priority, d.hot_priority) == (3, 2, 3)
-    assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == pytest.approx((0.25, 0.2, 0.0, 0.0))
-    assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (0.0, 0.0, 500.0, 400.0)
+    assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == pytest.approx((0.35, 0.3, 0.15, 0.0))
+    assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (400.0, 300.0, 400.0, 400.0)
     assert d.promote_big_scene == 60.0
+    assert (d.trace_group, d.trace_solo_bar, d.prepass_cap_split) == (4, pytest.approx(6.0), 0)
     assert d.occupancy_small == d.occupancy_low == d.occupancy_normal == 1.0
     lib = rtx.load_library()
     assert lib.rtx_set_schedule(None, C.byref(d)) == -1
