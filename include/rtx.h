@@ -219,7 +219,7 @@ typedef struct rtx_schedule {
     float tier1_bar_small;    /* default 1.6 */
     float tier1_bar_low;      /* default 2.0 */
     float tier2_bar_small;    /* default 2.0 */
-    float tier2_bar_medium;   /* default 1.2 */
+    float tier2_bar_medium;   /* default 1e30 (none; 1.2 in earlier builds) */
     float tier2_bar;          /* default 1e30 (no tier 2 for a larger part) */
     float small_share;        /* default 1.2 pixels per resident lane */
     float low_share;          /* default 2.5 */

@@ -97,7 +97,11 @@ constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than th
 constexpr double kHeavy1AlphaLow = 2.0;     // tier-1 bar for a low share (3.0 until round 4, 3.5 until R4b)
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
-constexpr double kHeavy2AlphaMedium = 1.2;  // tier 2 for a medium share: key > this * share (2-way split: 37 -> 34 ms, r5a-b)
+// tier 2 for a medium share: key > this * share (default: none). 1.2 until round 4 (2-way split 37 -> 34 ms
+// in r5a-b, before k_trace); with tier 1 in k_trace's pixel groups, tier-2 waves (8 rays, 8 lanes each: ~6x the
+// lane time per segment of lane mode) cost more throughput than they save: parts 4 20.4 -> 18.1 ms, parts 2
+// 28.4 -> 26.4 without them (profiles/R6p_tier2_sweep_r4_r2.jsonl)
+constexpr double kHeavy2AlphaMedium = 1e30;
 constexpr double kHeavy2AlphaLarge = 1e30;  // tier 2 for a larger share (default: none)
 // k_trace waves (tier 1 outside k_render) as a fraction of the resident waves, by share class.
 // Round 4 (k_trace traces 4 tier-1 pixels per wave, the heaviest alone; profiles/R6i_*, R6j_*): with

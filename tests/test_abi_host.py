@@ -105,7 +105,7 @@ def test_schedule_defaults_and_validation(rtx):
     d = rtx.schedule_defaults()
     assert d.tier1_bar == pytest.approx(1.7) and d.tier1_bar_small == pytest.approx(1.6)
     assert d.tier1_bar_low == pytest.approx(2.0) and d.tier2_bar_small == pytest.approx(2.0)
-    assert d.tier2_bar_medium == pytest.approx(1.2) and d.small_share == pytest.approx(1.2)
+    assert d.tier2_bar_medium == pytest.approx(1e30) and d.small_share == pytest.approx(1.2)
     assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
     assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 32 and d.tail_coop_max_large == 8
     assert d.refill_chunk == 16
