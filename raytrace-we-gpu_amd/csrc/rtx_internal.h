@@ -83,7 +83,9 @@ struct KParams {
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
-    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0 (NULL = none)
+    uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0
+                                   // [5] mean segments per pixel at the full spp (float bits) (NULL = none)
+    const uint32_t *cost_in;       // render: the pre-pass's per-pixel segments (dynamic wave priority; NULL = off)
     uint32_t trace_lg;             // k_trace: log2(lanes per pixel) of its waves past the solo slots [0, k0)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels

@@ -314,26 +314,22 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
     f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy};
     f2v vz = {T.vz, T.vz}, ku = {k0, k0}, kv = {k1, k1};
     const f2v th = {T.thr, T.thr};
-    // One 8-sphere block (blk(i) = its i-th float); true when some lane's
-    // list is full and the scan must stop after this block.
-    auto step = [&](auto blk, uint32_t bb) -> bool {
-        f2v q[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const f2v cx = {blk(2 * p), blk(2 * p + 1)};
-            const f2v cz = {blk(16 + 2 * p), blk(17 + 2 * p)};
-            const f2v R = {blk(24 + 2 * p), blk(25 + 2 * p)};
-            f2v pu, pv;
-            if constexpr (kFlat) {  // line_test_q_flat: c.v - o.v is one fma
-                pu = fma2(cx, ux, fma2(cz, uz, ku));
-                pv = fma2(cz, vz, kv);
-            } else {                // line_test_q
-                const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
-                pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, ku)));
-                pv = fma2(cy, vy, fma2(cz, vz, kv));
-            }
-            q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+    // Q of one sphere pair (cy unused on a flat run)
+    auto qpair = [&](f2v cx, f2v cy, f2v cz, f2v R) -> f2v {
+        f2v pu, pv;
+        if constexpr (kFlat) {  // line_test_q_flat: c.v - o.v is one fma
+            pu = fma2(cx, ux, fma2(cz, uz, ku));
+            pv = fma2(cz, vz, kv);
+        } else {                // line_test_q
+            pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, ku)));
+            pv = fma2(cy, vy, fma2(cz, vz, kv));
         }
+        return fma2(-pv, pv, fma2(-pu, pu, R));
+    };
+    // A block's four pair results q: the ballot, and each flagging lane's
+    // list entry; true when some lane's list is full and the scan must stop
+    // after this block.
+    auto finish = [&](const f2v *q, uint32_t bb) -> bool {
         // a chain, so that it folds into v_max3_f32
         const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
                                                  q[2].y), q[3].x), q[3].y);
@@ -356,6 +352,15 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             return __ballot(cnt == cand_of<kPF>()) != 0ull;
         }
         return false;
+    };
+    // One 8-sphere block (blk(i) = its i-th float)
+    auto step = [&](auto blk, uint32_t bb) -> bool {
+        f2v q[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+            q[p] = qpair(f2v{blk(2 * p), blk(2 * p + 1)}, kFlat ? f2v{0.0f, 0.0f} : f2v{blk(8 + 2 * p), blk(9 + 2 * p)},
+                         f2v{blk(16 + 2 * p), blk(17 + 2 * p)}, f2v{blk(24 + 2 * p), blk(25 + 2 * p)});
+        return finish(q, bb);
     };
     full = true;
     if (kPF && RTX_PF_RING && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
@@ -943,6 +948,18 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
 #ifndef RTX_PROM_EXACT_RATE  // A/B: a restarted pixel's promotion rate over its samples from 0 (1) or from cost_spp (0)
 #define RTX_PROM_EXACT_RATE 1
 #endif
+#ifndef RTX_DYN_PRIO  // lane mode: a wave's priority from its lanes' projected remaining segments (0: the
+#define RTX_DYN_PRIO 0    // static hot slots, rtx_schedule.hot_fraction)
+#endif
+#ifndef RTX_DYN_A1  // levels 1, 2, 3 above these multiples of the mean pixel's segments
+#define RTX_DYN_A1 0.75f
+#endif
+#ifndef RTX_DYN_A2
+#define RTX_DYN_A2 1.25f
+#endif
+#ifndef RTX_DYN_A3
+#define RTX_DYN_A3 2.0f
+#endif
 // Lane state: the pixel it is tracing and that pixel's current path.
 constexpr uint32_t kSeg0Restart = 0x80000000u;  // Lane::seg0 flag (a lane's segs stay far below 2^31)
 struct Lane {
@@ -953,6 +970,7 @@ struct Lane {
     uint32_t slot;       // its pixel-queue slot (priority of the heaviest pixels' waves)
     uint32_t seg0;       // segs when the pixel started (cost pre-pass: per-pixel segments);
                          // kSeg0Restart: the render restarted it from sample 0 (cost_cap)
+    uint32_t c0;         // the pre-pass's segments of a resumed pixel (dynamic priority; else 0)
     bool active;         // tracing a pixel
     uint32_t cb, ce;     // the wave's private run of queue slots (refill; wave-uniform)
 };
@@ -1301,10 +1319,12 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
     lane_pixel(P, gid, L.x, L.y);
     L.seg0 = L.segs;
     const float4 st = P.state && !P.cost_out ? P.state[gid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    L.c0 = 0u;
     if (P.state && !P.cost_out && !__builtin_isnan(st.w)) {  // after the pre-pass's cost_spp samples (identical state)
         L.acc = mk3(st.x, st.y, st.z);
         L.sample = P.cost_spp;
         L.seed = st.w;
+        if (RTX_DYN_PRIO && P.cost_in) L.c0 = P.cost_in[gid];
     } else {  // a fresh pixel, or one the pre-pass stopped (cost_cap)
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
@@ -1582,7 +1602,7 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
     mvf(W.acc.x); mvf(W.acc.y); mvf(W.acc.z);
     mvf(W.a); mvf(W.inv_a); mvf(W.seed);
     mvu(W.sample); mvu(W.bounce); mvu(W.segs);
-    mvu(W.x); mvu(W.y); mvu(W.gid); mvu(W.slot); mvu(W.seg0);
+    mvu(W.x); mvu(W.y); mvu(W.gid); mvu(W.slot); mvu(W.seg0); mvu(W.c0);
     W.active = has;
 }
 
@@ -1721,6 +1741,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
+    const float dyn_m = (RTX_DYN_PRIO && kPersist && P.cost_in && P.heavy) ? __uint_as_float(P.heavy[5]) : 0.0f;
     // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
     const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
     uint32_t written = 0;  // pixels this wave wrote since it last reported
@@ -1784,7 +1805,24 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
-        set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
+        if (RTX_DYN_PRIO && P.cost_in) {
+            // the wave's priority: its longest projected remaining chain
+            // (segments per sample so far, the pre-pass's included, times the
+            // samples left) against the mean pixel (heavy[5]); a pixel the
+            // pre-pass stopped counts as long until its first sample ends
+            float rem = 0.0f;
+            if (L.active) {
+                const bool rs = (L.seg0 & kSeg0Restart) != 0u;
+                const float segs = (float)(L.segs - (L.seg0 & ~kSeg0Restart) + L.c0);
+                rem = rs && L.sample == 0u ? 3.0e38f : segs * (float)(P.spp - L.sample) / (float)max(L.sample, 1u);
+            }
+            set_prio(__ballot(rem > RTX_DYN_A3 * dyn_m) != 0ull   ? 3u
+                     : __ballot(rem > RTX_DYN_A2 * dyn_m) != 0ull ? 2u
+                     : __ballot(rem > RTX_DYN_A1 * dyn_m) != 0ull ? 1u
+                                                                  : 0u);
+        } else {
+            set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
+        }
         bool promoted = false;
         if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
             float best = __uint_as_float(0x7f800000u);
@@ -1895,7 +1933,7 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
 }
 
 // Tier 1 as its own kernel (the scheduled path, scenes up to kCoopLds
-// spheres): single-wave workgroups launched on the context's auxiliary
+// spheres): workgroups of independent waves launched on the context's auxiliary
 // stream beside k_render (launch_render), taking tier-1 slots ([0, k1) of the
 // cost-ordered queue, k_heavy_split) and tracing each pixel with a group of
 // lanes (trace_group_segment), at wave priority prio_t1. The very heaviest
@@ -1909,7 +1947,11 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
 // VGPRs) keeps this state out of k_render, whose lane-mode loop it would
 // otherwise crowd into scratch. k_render skips tier 1
 // (KParams::trace_ext).
-constexpr uint32_t kTraceThreads = 64;
+// Four independent waves per workgroup (no barrier after the copy): they share
+// one LDS copy of the scene. One-wave workgroups, each with its own 10-13 KiB
+// copy, took LDS the render's blocks needed: at R = 8 (7 k_trace waves per
+// CU) only ~79 % of k_render's lanes were resident (profiles/R6r_pixel_timelines.jsonl).
+constexpr uint32_t kTraceThreads = 256;
 __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem), true, kTraceThreads);
@@ -2142,7 +2184,7 @@ KTune default_tune() {
     return t;
 }
 namespace {
-__global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t *heavy,
+__global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t lanes, uint32_t spp, uint32_t *heavy,
                               const KTune t) {
     if (threadIdx.x != 0u) return;
     double w = 0.0;
@@ -2168,6 +2210,8 @@ __global__ void k_heavy_split(const uint32_t *counts, uint32_t npix, uint32_t la
     heavy[1] = kh;
     heavy[3] = k1;
     heavy[4] = k0;
+    // the mean pixel's segments at the full spp (keys: 9 one-sample costs; saturated keys count as the top bucket)
+    heavy[5] = __float_as_uint((float)(w / (double)(npix ? npix : 1u) / 9.0 * (double)spp));
 }
 
 // ---- per-sample RNG (rtx_frame.rng_mode 1): one lane per (pixel, sample) --
@@ -2681,8 +2725,8 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         blocks = max(1u, (uint32_t)(blocks * occ + 0.5));
     }
     uint32_t *heavy = sched.buckets + 2 * kCostBuckets;
-    hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, heavy,
-                       tune);
+    hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, p.spp,
+                       heavy, tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                        p.rows_local, c.spp, split_cap, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
     KParams q = p;
@@ -2691,6 +2735,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
+    q.cost_in = RTX_DYN_PRIO ? sched.cost : nullptr;
     // private queue runs per wave for a large part only (a whole frame: R = 2,
     // 4, 8 shares measured no better, profiles/R3x_parts.jsonl)
     // and small scenes only (at 100k spheres a pixel takes ~100 ms in lane
@@ -2733,7 +2778,8 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         e = hipEventRecord(sched.ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(sched.aux, sched.ev_fork, 0);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_trace, dim3(trace_waves), dim3(kTraceThreads), tlds, sched.aux, q);
+        hipLaunchKernelGGL(k_trace, dim3((trace_waves + kTraceThreads / 64u - 1u) / (kTraceThreads / 64u)), dim3(kTraceThreads), tlds,
+                           sched.aux, q);
         e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(sched.ev_join, sched.aux);
         if (e != hipSuccess) return e;

@@ -76,10 +76,20 @@ for R in a.parts:
                              "us_per_segment_max": round(float(ups[sel].max()), 3),
                              "start_us_max": round(float(s_us[sel].max()), 1),
                              "end_us_max": round(float(e_us[sel].max()), 1)}
+    # over time (1 ms bins): pixels in flight per mode and their segment rate
+    # (segments per us, each pixel at its own mean rate): how the share's
+    # throughput falls off towards its end
+    prof = []
+    rate = np.where(ok & (dur > 0), seg / np.maximum(dur, 1e-3), 0.0)
+    for tc in np.arange(0.5e3, span, 1e3):
+        on = ok & (s_us <= tc) & (e_us > tc)
+        prof.append({"t_ms": round(float(tc) / 1e3, 1),
+                     "active": {str(m): int((on & (mode == m)).sum()) for m in (0, 1, 2, 3)},
+                     "seg_per_us": {str(m): round(float(rate[on & (mode == m)].sum()), 1) for m in (0, 1, 2, 3)}})
     late = ok & (e_us > 0.9 * span)
     out = {"set": a.set or "default", "parts": R, "part": p, "pixels": npix, "kernel_ms": round(st.kernel_ms / max(1, st.launches), 3),
            "span_us": round(span, 1), "segments_total": int(seg.sum()), "segments_max": int(seg.max()),
-           "modes": modes, "last_finishing": [rec(i) for i in last], "heaviest": [rec(i) for i in heavy],
+           "modes": modes, "profile": prof, "last_finishing": [rec(i) for i in last], "heaviest": [rec(i) for i in heavy],
            "late10pct": {"pixels": int(late.sum()), "segments_mean": round(float(seg[late].mean()), 1) if late.any() else 0,
                          "start_us_mean": round(float(s_us[late].mean()), 1) if late.any() else 0}}
     print(json.dumps(out), flush=True)
