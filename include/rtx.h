@@ -38,8 +38,11 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 130 /* 1.3.0 */
+#define RTX_VERSION 140 /* 1.4.0 */
 /* ABI notes.
+ *  1.4.0: rtx_schedule.prio_bar1..3 (after prepass_cap_split, before
+ *         `reserved`): dynamic lane-mode wave priority; the struct grew by
+ *         12 bytes.
  *  1.3.0: rtx_schedule.trace_solo_bar (after promote_big_scene),
  *         trace_group and prepass_cap_split (after refill_chunk): the
  *         struct grew by 12 bytes;
@@ -210,7 +213,14 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     many consecutive slots of the cost-ordered queue, re-stocked when
  *     empty, so its lanes hold pixels from few runs (coherent rays) rather
  *     than one slot per refill from wherever the queue head is; the last
- *     eighth of the queue is taken slot by slot.
+ *     eighth of the queue is taken slot by slot;
+ *   - prio_bar1..3: a lane-mode wave runs at priority 1, 2 or 3 while some
+ *     lane's pixel is projected (its segments per sample so far, the cost
+ *     pre-pass's included, times the samples left) to need more than
+ *     prio_barK x the mean pixel's segments (the pre-pass's estimate), else
+ *     at 0: the longest remaining chains get the SIMDs' issue, whatever their
+ *     key said; prio_bar1 = 0 selects the static scheme instead (hot_fraction
+ *     of the queue's first slots at hot_priority).
  * Results never depend on the schedule (every pixel's operations are the
  * same whichever lanes trace it); only the time does. The defaults are the
  * measured best. A context starts with the defaults. */
@@ -249,6 +259,9 @@ typedef struct rtx_schedule {
     uint32_t prepass_cap_split; /* default 0 (none): a row-split part's cost pre-pass stops a pixel past this
                                    many segments (0..4096); it goes to the top of the queue (tier 1) and the
                                    render traces it from sample 0 */
+    float prio_bar1;          /* default 0.5 (0: static hot slots, hot_fraction / hot_priority) */
+    float prio_bar2;          /* default 1.0 */
+    float prio_bar3;          /* default 1.5 */
     uint32_t reserved;        /* must be 0 */
 } rtx_schedule;
 /* The library's defaults (no context, no GPU). */
@@ -258,7 +271,8 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
  * tail_coop_max and tail_coop_max_large in 1..64,
  * priorities in 0..3, refill_chunk in 0..4096, trace_group 1, 2 or 4,
- * trace_solo_bar > 0, prepass_cap_split in 0..4096, reserved 0. */
+ * trace_solo_bar > 0, prepass_cap_split in 0..4096, prio_bar1 = 0 or
+ * 0 < prio_bar1 <= prio_bar2 <= prio_bar3 <= 1e30, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);
 RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 

@@ -298,6 +298,9 @@ int rtx_schedule_defaults(rtx_schedule *out) {
     out->trace_group = t.trace_group;
     out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
     out->prepass_cap_split = t.cap_split;
+    out->prio_bar1 = (float)t.dyn1;
+    out->prio_bar2 = (float)t.dyn2;
+    out->prio_bar3 = (float)t.dyn3;
     return RTX_OK;
 }
 
@@ -338,6 +341,9 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_group must be 1, 2 or 4");
     if (s->prepass_cap_split > 4096)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: prepass_cap_split must be in 0..4096");
+    if (!(s->prio_bar1 == 0.0f || (s->prio_bar1 > 0.0f && s->prio_bar1 <= s->prio_bar2 &&
+                                   s->prio_bar2 <= s->prio_bar3 && s->prio_bar3 <= 1e30f)))
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: prio_bar1..3 must be 0 or 0 < bar1 <= bar2 <= bar3 <= 1e30");
     if (s->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_set_schedule: reserved must be 0");
     rtx::KTune t;
     t.a1 = s->tier1_bar;
@@ -371,6 +377,9 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     t.trace_group = s->trace_group;
     t.trace_solo = s->trace_solo_bar;
     t.cap_split = s->prepass_cap_split;
+    t.dyn1 = s->prio_bar1;
+    t.dyn2 = s->prio_bar1 > 0.0f ? s->prio_bar2 : 0.0f;
+    t.dyn3 = s->prio_bar1 > 0.0f ? s->prio_bar3 : 0.0f;
     c->tune = t;
     return RTX_OK;
 }
@@ -410,6 +419,9 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     out->trace_group = t.trace_group;
     out->trace_solo_bar = (float)std::min(t.trace_solo, 1e30);
     out->prepass_cap_split = t.cap_split;
+    out->prio_bar1 = (float)t.dyn1;
+    out->prio_bar2 = (float)t.dyn2;
+    out->prio_bar3 = (float)t.dyn3;
     return RTX_OK;
 }
 

@@ -86,6 +86,7 @@ struct KParams {
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0
                                    // [5] mean segments per pixel at the full spp (float bits) (NULL = none)
     const uint32_t *cost_in;       // render: the pre-pass's per-pixel segments (dynamic wave priority; NULL = off)
+    float dyn_bar[3];              // ... its bars (x heavy[5])
     uint32_t trace_lg;             // k_trace: log2(lanes per pixel) of its waves past the solo slots [0, k0)
     // per-sample RNG kernel (k_render_ps): per-wave sample-colour scratch
     // [wave][kPsSlots][ps_cap] float4, batches of at most ps_px pixels
@@ -115,6 +116,7 @@ struct KTune {
     uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2, 4, 8)
     double trace_solo;                                         // ... one per wave above this x share (k0)
     uint32_t cap_split;                                        // pre-pass cap of a row-split part (0: none)
+    double dyn1, dyn2, dyn3;  // lane-mode wave priority 1/2/3 above these x the mean pixel (dyn1 0: static hot slots)
 };
 KTune default_tune();
 

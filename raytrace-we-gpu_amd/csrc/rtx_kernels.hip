@@ -123,6 +123,13 @@ constexpr uint32_t kTraceGroup = 4;
 constexpr double kTraceSolo = 6.0;
 // pre-pass segment cap for row-split parts (0: none; see launch_render)
 constexpr uint32_t kCapSplit = 0;
+// Lane-mode wave priority from the lanes' projected remaining chains (k_render,
+// rtx_schedule.prio_bar*): levels 1/2/3 above these x the mean pixel's
+// segments. Against the static hot slots (the queue's first 20 % of the
+// resident lanes at priority 3): parts 2 26.4-27.0 -> 25.9-26.0 ms, parts 4
+// 18.4-18.9 -> 17.6-17.7, parts 8 13.6 -> 13.2, the whole frame flat (0.75/1.25/2:
+// parts 8 slower; 0.25/0.5/1 and 0.35/0.7/1.1: parts 4 slower; profiles/R6t_*, R6u_*)
+constexpr double kDynPrio1 = 0.5, kDynPrio2 = 1.0, kDynPrio3 = 1.5;
 // Cost pre-pass cap (whole-frame parts only: in a row-split share a capped,
 // under-rated key keeps heavy pixels out of the tiers — parts 2/4/8 30/21/15
 // -> 34/26/26 ms, profiles/R4h_parts.jsonl): a pixel still tracing after
@@ -136,6 +143,9 @@ constexpr uint32_t kCapSplit = 0;
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
+#ifndef RTX_DYN_TAIL  // A/B: a coop-tail wave also takes the dynamic priority (rtx_schedule.prio_bar*) when higher
+#define RTX_DYN_TAIL 0
+#endif
 constexpr uint32_t kRB = 256;           // threads per render workgroup
 #ifndef RTX_WAVES_PER_SIMD
 #define RTX_WAVES_PER_SIMD 5  // occupancy request for the render kernels: 96 VGPRs (the compiler's own
@@ -948,18 +958,6 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
 #ifndef RTX_PROM_EXACT_RATE  // A/B: a restarted pixel's promotion rate over its samples from 0 (1) or from cost_spp (0)
 #define RTX_PROM_EXACT_RATE 1
 #endif
-#ifndef RTX_DYN_PRIO  // lane mode: a wave's priority from its lanes' projected remaining segments (0: the
-#define RTX_DYN_PRIO 0    // static hot slots, rtx_schedule.hot_fraction)
-#endif
-#ifndef RTX_DYN_A1  // levels 1, 2, 3 above these multiples of the mean pixel's segments
-#define RTX_DYN_A1 0.75f
-#endif
-#ifndef RTX_DYN_A2
-#define RTX_DYN_A2 1.25f
-#endif
-#ifndef RTX_DYN_A3
-#define RTX_DYN_A3 2.0f
-#endif
 // Lane state: the pixel it is tracing and that pixel's current path.
 constexpr uint32_t kSeg0Restart = 0x80000000u;  // Lane::seg0 flag (a lane's segs stay far below 2^31)
 struct Lane {
@@ -1324,7 +1322,7 @@ __device__ __forceinline__ void start_pixel(const KParams &P, const Frame &F, ui
         L.acc = mk3(st.x, st.y, st.z);
         L.sample = P.cost_spp;
         L.seed = st.w;
-        if (RTX_DYN_PRIO && P.cost_in) L.c0 = P.cost_in[gid];
+        if (P.cost_in) L.c0 = P.cost_in[gid];
     } else {  // a fresh pixel, or one the pre-pass stopped (cost_cap)
         L.acc = mk3(0.0f, 0.0f, 0.0f);
         L.sample = 0;
@@ -1343,6 +1341,24 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
         case 2: __builtin_amdgcn_s_setprio(2); break;
         default: __builtin_amdgcn_s_setprio(3); break;
     }
+}
+
+// Dynamic lane-mode wave priority (KParams::cost_in, rtx_schedule.prio_bar*):
+// the wave's longest projected remaining chain (segments per sample so far,
+// the pre-pass's included, times the samples left) against the bars x the
+// mean pixel's segments m; a pixel the pre-pass stopped counts as long until
+// its first sample ends.
+__device__ __forceinline__ uint32_t dyn_level(const KParams &P, const Lane &L, float m) {
+    float rem = 0.0f;
+    if (L.active) {
+        const bool rs = (L.seg0 & kSeg0Restart) != 0u;
+        const float segs = (float)(L.segs - (L.seg0 & ~kSeg0Restart) + L.c0);
+        rem = rs && L.sample == 0u ? 3.0e38f : segs * (float)(P.spp - L.sample) / (float)max(L.sample, 1u);
+    }
+    return __ballot(rem > P.dyn_bar[2] * m) != 0ull   ? 3u
+           : __ballot(rem > P.dyn_bar[1] * m) != 0ull ? 2u
+           : __ballot(rem > P.dyn_bar[0] * m) != 0ull ? 1u
+                                                      : 0u;
 }
 
 // Persistent-lane pixel queue: every idle lane of the wave takes the next
@@ -1741,7 +1757,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     H.t2_done = H.k1 == H.kh;
     H.tier = 0;
     const uint32_t kh = H.kh;
-    const float dyn_m = (RTX_DYN_PRIO && kPersist && P.cost_in && P.heavy) ? __uint_as_float(P.heavy[5]) : 0.0f;
+    // the mean pixel's segments (dynamic priority's unit)
+    const float dyn_m = (kPersist && P.cost_in && P.heavy) ? __uint_as_float(P.heavy[5]) : 0.0f;
     // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
     const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
     uint32_t written = 0;  // pixels this wave wrote since it last reported
@@ -1777,7 +1794,10 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             float my_best = __uint_as_float(0x7f800000u);
             bool my_seq = false;
             // this wave carries the frame's critical path: tier 1 > tier 2 > tail
-            set_prio(H.tier == 1u ? P.prio_t1 : H.tier == 2u ? P.prio_t2 : (uint32_t)kTailPrio);
+            set_prio(H.tier == 1u   ? P.prio_t1
+                     : H.tier == 2u ? P.prio_t2
+                     : (RTX_DYN_TAIL && P.cost_in) ? max((uint32_t)kTailPrio, dyn_level(P, L, dyn_m))
+                                                   : (uint32_t)kTailPrio);
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
             bool promoted = false;
@@ -1805,21 +1825,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         // lane mode: a wave that holds one of the heaviest pixels of the
         // normal queue (its first prio_slots slots) runs at the top priority,
         // so its time per segment is not stretched by the SIMD's other waves
-        if (RTX_DYN_PRIO && P.cost_in) {
-            // the wave's priority: its longest projected remaining chain
-            // (segments per sample so far, the pre-pass's included, times the
-            // samples left) against the mean pixel (heavy[5]); a pixel the
-            // pre-pass stopped counts as long until its first sample ends
-            float rem = 0.0f;
-            if (L.active) {
-                const bool rs = (L.seg0 & kSeg0Restart) != 0u;
-                const float segs = (float)(L.segs - (L.seg0 & ~kSeg0Restart) + L.c0);
-                rem = rs && L.sample == 0u ? 3.0e38f : segs * (float)(P.spp - L.sample) / (float)max(L.sample, 1u);
-            }
-            set_prio(__ballot(rem > RTX_DYN_A3 * dyn_m) != 0ull   ? 3u
-                     : __ballot(rem > RTX_DYN_A2 * dyn_m) != 0ull ? 2u
-                     : __ballot(rem > RTX_DYN_A1 * dyn_m) != 0ull ? 1u
-                                                                  : 0u);
+        if (P.cost_in) {
+            set_prio(dyn_level(P, L, dyn_m));
         } else {
             set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
         }
@@ -2181,6 +2188,9 @@ KTune default_tune() {
     t.trace_group = kTraceGroup;
     t.trace_solo = kTraceSolo;
     t.cap_split = kCapSplit;
+    t.dyn1 = kDynPrio1;
+    t.dyn2 = kDynPrio2;
+    t.dyn3 = kDynPrio3;
     return t;
 }
 namespace {
@@ -2735,7 +2745,12 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
-    q.cost_in = RTX_DYN_PRIO ? sched.cost : nullptr;
+    if (tune.dyn1 > 0.0) {  // dynamic lane-mode wave priority (rtx_schedule.prio_bar*)
+        q.cost_in = sched.cost;
+        q.dyn_bar[0] = (float)tune.dyn1;
+        q.dyn_bar[1] = (float)tune.dyn2;
+        q.dyn_bar[2] = (float)tune.dyn3;
+    }
     // private queue runs per wave for a large part only (a whole frame: R = 2,
     // 4, 8 shares measured no better, profiles/R3x_parts.jsonl)
     // and small scenes only (at 100k spheres a pixel takes ~100 ms in lane

@@ -27,7 +27,7 @@ LIB_PATH = os.environ.get("RTX_LIB", os.path.join(_PKG_DIR, "lib", "librtx.so"))
 
 RTX_OK = 0
 RTX_ERR_INCOMPLETE = -5  # a render launch left pixels unwritten (ABI 1.3)
-SCHEDULE_ABI = 130  # the rtx_schedule layout this module passes (ABI 1.3.0)
+SCHEDULE_ABI = 140  # the rtx_schedule layout this module passes (ABI 1.4.0)
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
@@ -67,7 +67,8 @@ class rtx_schedule(C.Structure):
                 ("trace_solo_bar", C.c_float),
                 ("tail_coop_max", C.c_uint32), ("tail_coop_max_large", C.c_uint32), ("tier1_priority", C.c_uint32), ("tier2_priority", C.c_uint32),
                 ("hot_priority", C.c_uint32), ("refill_chunk", C.c_uint32), ("trace_group", C.c_uint32),
-                ("prepass_cap_split", C.c_uint32), ("reserved", C.c_uint32)]
+                ("prepass_cap_split", C.c_uint32), ("prio_bar1", C.c_float), ("prio_bar2", C.c_float),
+                ("prio_bar3", C.c_float), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
@@ -264,9 +265,9 @@ def part_row_ids(height: int, tile_rows: int, part: int, nparts: int) -> np.ndar
 
 
 def _require_schedule_abi(lib: C.CDLL):
-    """rtx_schedule grew in 1.2.0 (promote_big_scene, refill_chunk) and
-    1.3.0 (trace_solo_bar, trace_group): an older library would read this
-    module's struct at the wrong offsets."""
+    """rtx_schedule grew in 1.2.0 (promote_big_scene, refill_chunk), 1.3.0
+    (trace_solo_bar, trace_group) and 1.4.0 (prio_bar1..3): an older library
+    would read this module's struct at the wrong offsets."""
     v = int(lib.rtx_version())
     if v < SCHEDULE_ABI or not hasattr(lib, "rtx_set_schedule"):
         raise RtxError(f"library ABI {v} predates the rtx_schedule layout {SCHEDULE_ABI} this binding passes")

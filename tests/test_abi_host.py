@@ -50,7 +50,7 @@ def test_library_built_for_gfx950(rtx):
 
 def test_version_and_error_paths(rtx):
     lib = rtx.load_library()
-    assert lib.rtx_version() == 130
+    assert lib.rtx_version() == 140
     # null arguments are rejected without touching the GPU
     assert lib.rtx_upload_world(None, None) == -1
     assert b"null" in lib.rtx_last_error()
@@ -115,6 +115,7 @@ def test_schedule_defaults_and_validation(rtx):
     assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (400.0, 300.0, 400.0, 400.0)
     assert d.promote_big_scene == 60.0
     assert (d.trace_group, d.trace_solo_bar, d.prepass_cap_split) == (4, pytest.approx(6.0), 0)
+    assert (d.prio_bar1, d.prio_bar2, d.prio_bar3) == pytest.approx((0.5, 1.0, 1.5))
     assert d.occupancy_small == d.occupancy_low == d.occupancy_normal == 1.0
     lib = rtx.load_library()
     assert lib.rtx_set_schedule(None, C.byref(d)) == -1
@@ -163,7 +164,7 @@ def test_schedule_calls_refuse_an_older_abi(rtx):
     promote_large at the wrong offsets) instead of installing a wrong schedule."""
     class OldLib:
         def rtx_version(self):
-            return 110
+            return 130
 
         def rtx_set_schedule(self, *a):
             raise AssertionError("must not be called")

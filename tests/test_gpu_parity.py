@@ -797,6 +797,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
                        ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_group", 0), ("trace_group", 3), ("trace_group", 8), ("trace_solo_bar", 0.0), ("prepass_cap_split", 5000), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
+                       ("prio_bar1", -1.0), ("prio_bar1", 2.0), ("prio_bar2", 0.2), ("prio_bar3", float("nan")),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
             gpu_ctx.set_schedule(**{field: bad})
@@ -817,7 +818,10 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
                 dict(trace_small=0.5, trace_low=0.5, trace_medium=0.5, trace_large=0.5, tier1_bar=0.01,
                      tier1_bar_small=0.01, tier1_bar_low=0.01),
                 dict(trace_small=0.5, trace_low=0.5, trace_medium=0.5, trace_large=0.5, tier1_bar=0.01,
-                     tier1_bar_small=0.01, tier1_bar_low=0.01, trace_group=4, trace_solo_bar=0.5)]
+                     tier1_bar_small=0.01, tier1_bar_low=0.01, trace_group=4, trace_solo_bar=0.5),
+                dict(prio_bar1=0.0),  # the static hot slots
+                dict(prio_bar1=1e-3, prio_bar2=1e-3, prio_bar3=1e-3),  # every lane-mode wave at priority 3
+                dict(prio_bar1=1e30, prio_bar2=1e30, prio_bar3=1e30)]  # ... at 0
     for ex in extremes:
         gpu_ctx.set_schedule()
         gpu_ctx.set_schedule(**ex)

@@ -8,7 +8,7 @@ SHORT = {"a1": "tier1_bar", "a1s": "tier1_bar_small", "a1l": "tier1_bar_low", "a
          "trm": "trace_medium", "trL": "trace_large", "prs": "promote_small", "prl": "promote_low",
          "prm": "promote_medium", "prL": "promote_large", "prB": "promote_big_scene", "p2": "tier2_priority", "ph": "hot_priority",
          "chunk": "refill_chunk", "tg": "trace_group", "tsolo": "trace_solo_bar",
-         "capS": "prepass_cap_split"}
+         "capS": "prepass_cap_split", "pb1": "prio_bar1", "pb2": "prio_bar2", "pb3": "prio_bar3"}
 
 
 def schedule_of(setting):
