@@ -143,6 +143,9 @@ constexpr double kDynPrio1 = 0.5, kDynPrio2 = 1.0, kDynPrio3 = 1.5;
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
+#ifndef RTX_EARLY_PROM  // A/B: a lane-mode pixel projected past this x the mean pixel may be promoted before
+#define RTX_EARLY_PROM 0    // its wave's queue is exhausted (0: never)
+#endif
 #ifndef RTX_DYN_TAIL  // A/B: a coop-tail wave also takes the dynamic priority (rtx_schedule.prio_bar*) when higher
 #define RTX_DYN_TAIL 0
 #endif
@@ -1221,14 +1224,14 @@ __device__ __forceinline__ void agent_store_order() {
 // published with agent-scope atomics (the consumer may sit on another XCD,
 // whose L2 does not see these stores otherwise): the fields, a wait for their
 // completion, then the epoch word (agent_store_order).
-__device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
+__device__ __forceinline__ bool promote(const KParams &P, const Lane &L, uint32_t min_segs) {
     // samples traced in this launch (>= 1 here): after the pre-pass's
     // cost_spp, or from sample 0 for a pixel the pre-pass stopped (cost_cap;
     // kSeg0Restart in seg0)
     const bool restarted = RTX_PROM_EXACT_RATE && (L.seg0 & kSeg0Restart) != 0u;
     const uint32_t done = max(restarted ? L.sample : L.sample - min(L.sample, P.cost_spp), 1u);
     const uint32_t segs = L.segs - (L.seg0 & ~kSeg0Restart);
-    if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)P.prom_min * done) return false;
+    if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)min_segs * done) return false;
     const uint32_t slot = atomicAdd(&P.prom[0], 1u);
     if (slot >= P.prom_cap) return false;  // queue full: the lane keeps its pixel
     uint32_t *e = P.prom_q + 8u * slot;
@@ -1249,7 +1252,7 @@ __device__ __forceinline__ bool promote(const KParams &P, const Lane &L) {
 // exhausted and promotion is on. Returns true when the pixel was promoted.
 template <bool kCost = false>
 __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L, int hit, float t,
-                                      bool may_promote = false) {
+                                      bool may_promote = false, uint32_t early_min = 0u) {
     L.segs++;
     f3 c;
     const int r = path_segment(P, L, hit, t, c);
@@ -1261,7 +1264,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L,
             write_pixel<kCost>(P, L);
             L.active = false;
             diag_pixel_end(P, L.gid);
-        } else if (!kCost && may_promote && promote(P, L)) {
+        } else if (!kCost && (may_promote || early_min != 0u) && promote(P, L, may_promote ? P.prom_min : early_min)) {
             L.active = false;  // the promotion queue owns the pixel now
             return true;
         } else {
@@ -1759,6 +1762,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const uint32_t kh = H.kh;
     // the mean pixel's segments (dynamic priority's unit)
     const float dyn_m = (kPersist && P.cost_in && P.heavy) ? __uint_as_float(P.heavy[5]) : 0.0f;
+    // A/B: promotion before the queue is exhausted, above RTX_EARLY_PROM x the mean pixel
+    const uint32_t early_prom = (RTX_EARLY_PROM > 0 && prom_on && P.cost_in) ? (uint32_t)(RTX_EARLY_PROM * dyn_m) + 1u : 0u;
     // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
     const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
     uint32_t written = 0;  // pixels this wave wrote since it last reported
@@ -1836,7 +1841,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
             D.section(1);
-            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
+            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted, early_prom);
         } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
@@ -1847,7 +1852,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
-            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted);
+            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted, early_prom);
         }
         D.section(2);
         if (prom_on)  // pixels written this iteration (promoted ones are counted by whoever finishes them)
