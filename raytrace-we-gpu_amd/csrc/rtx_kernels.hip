@@ -146,6 +146,9 @@ constexpr int kTailPrio = 1;            // wave priority of a normal wave in its
 #ifndef RTX_EARLY_PROM  // A/B: a lane-mode pixel projected past this x the mean pixel may be promoted before
 #define RTX_EARLY_PROM 0    // its wave's queue is exhausted (0: never)
 #endif
+#ifndef RTX_TAIL_PROM  // A/B: a coop-tail wave with <= 8 pixels left promotes those projected past this many
+#define RTX_TAIL_PROM 0    // segments (0: prom_min only)
+#endif
 #ifndef RTX_DYN_TAIL  // A/B: a coop-tail wave also takes the dynamic priority (rtx_schedule.prio_bar*) when higher
 #define RTX_DYN_TAIL 0
 #endif
@@ -1248,11 +1251,13 @@ __device__ __forceinline__ bool promote(const KParams &P, const Lane &L, uint32_
 
 // Chain-RNG lane: one segment, then the pixel's next sample when the path
 // ends (acc += colour in sample order, :269-284), or the pixel's output
-// after its last sample (clears `active`). may_promote: the wave's queue is
-// exhausted and promotion is on. Returns true when the pixel was promoted.
+// after its last sample (clears `active`). prom_thr (0: none): promote the
+// pixel at a sample boundary if it is projected to need more segments than
+// this (KParams::prom_min once the wave's queue is exhausted). Returns true
+// when the pixel was promoted.
 template <bool kCost = false>
 __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L, int hit, float t,
-                                      bool may_promote = false, uint32_t early_min = 0u) {
+                                      uint32_t prom_thr = 0u) {
     L.segs++;
     f3 c;
     const int r = path_segment(P, L, hit, t, c);
@@ -1264,7 +1269,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const Frame &F, Lane &L,
             write_pixel<kCost>(P, L);
             L.active = false;
             diag_pixel_end(P, L.gid);
-        } else if (!kCost && (may_promote || early_min != 0u) && promote(P, L, may_promote ? P.prom_min : early_min)) {
+        } else if (!kCost && prom_thr != 0u && promote(P, L, prom_thr)) {
             L.active = false;  // the promotion queue owns the pixel now
             return true;
         } else {
@@ -1818,7 +1823,9 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 // the tail's pixels may be promoted (tier-1 waves already
                 // trace one ray with every lane; promoting tier-2 pixels
                 // measured 1-6 ms slower at R = 2, 4, 8: profiles/R3r_*)
-                promoted = shade<kCost>(P, F, L, min(my_hit, last), my_best, prom_on && exhausted && H.tier == 0u);
+                uint32_t thr = prom_on && exhausted && H.tier == 0u ? P.prom_min : 0u;
+                if (RTX_TAIL_PROM > 0 && thr != 0u && (uint32_t)__popcll(act) <= 8u) thr = min(thr, (uint32_t)RTX_TAIL_PROM);
+                promoted = shade<kCost>(P, F, L, min(my_hit, last), my_best, thr);
             }
             if (prom_on)
                 written += (uint32_t)__popcll(act & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
@@ -1841,7 +1848,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
             D.section(1);
-            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted, early_prom);
+            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : early_prom);
         } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
@@ -1852,7 +1859,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
-            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted, early_prom);
+            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : early_prom);
         }
         D.section(2);
         if (prom_on)  // pixels written this iteration (promoted ones are counted by whoever finishes them)
