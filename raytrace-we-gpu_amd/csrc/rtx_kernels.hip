@@ -143,15 +143,6 @@ constexpr double kDynPrio1 = 0.5, kDynPrio2 = 1.0, kDynPrio3 = 1.5;
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
-#ifndef RTX_EARLY_PROM  // A/B: a lane-mode pixel projected past this x the mean pixel may be promoted before
-#define RTX_EARLY_PROM 0    // its wave's queue is exhausted (0: never)
-#endif
-#ifndef RTX_TAIL_PROM  // A/B: a coop-tail wave with <= 8 pixels left promotes those projected past this many
-#define RTX_TAIL_PROM 0    // segments (0: prom_min only)
-#endif
-#ifndef RTX_DYN_TAIL  // A/B: a coop-tail wave also takes the dynamic priority (rtx_schedule.prio_bar*) when higher
-#define RTX_DYN_TAIL 0
-#endif
 constexpr uint32_t kRB = 256;           // threads per render workgroup
 #ifndef RTX_WAVES_PER_SIMD
 #define RTX_WAVES_PER_SIMD 5  // occupancy request for the render kernels: 96 VGPRs (the compiler's own
@@ -1767,8 +1758,6 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     const uint32_t kh = H.kh;
     // the mean pixel's segments (dynamic priority's unit)
     const float dyn_m = (kPersist && P.cost_in && P.heavy) ? __uint_as_float(P.heavy[5]) : 0.0f;
-    // A/B: promotion before the queue is exhausted, above RTX_EARLY_PROM x the mean pixel
-    const uint32_t early_prom = (RTX_EARLY_PROM > 0 && prom_on && P.cost_in) ? (uint32_t)(RTX_EARLY_PROM * dyn_m) + 1u : 0u;
     // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
     const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
     uint32_t written = 0;  // pixels this wave wrote since it last reported
@@ -1804,10 +1793,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             float my_best = __uint_as_float(0x7f800000u);
             bool my_seq = false;
             // this wave carries the frame's critical path: tier 1 > tier 2 > tail
-            set_prio(H.tier == 1u   ? P.prio_t1
-                     : H.tier == 2u ? P.prio_t2
-                     : (RTX_DYN_TAIL && P.cost_in) ? max((uint32_t)kTailPrio, dyn_level(P, L, dyn_m))
-                                                   : (uint32_t)kTailPrio);
+            set_prio(H.tier == 1u ? P.prio_t1 : H.tier == 2u ? P.prio_t2 : (uint32_t)kTailPrio);
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
             bool promoted = false;
@@ -1823,9 +1809,8 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                 // the tail's pixels may be promoted (tier-1 waves already
                 // trace one ray with every lane; promoting tier-2 pixels
                 // measured 1-6 ms slower at R = 2, 4, 8: profiles/R3r_*)
-                uint32_t thr = prom_on && exhausted && H.tier == 0u ? P.prom_min : 0u;
-                if (RTX_TAIL_PROM > 0 && thr != 0u && (uint32_t)__popcll(act) <= 8u) thr = min(thr, (uint32_t)RTX_TAIL_PROM);
-                promoted = shade<kCost>(P, F, L, min(my_hit, last), my_best, thr);
+                promoted = shade<kCost>(P, F, L, min(my_hit, last), my_best,
+                                        prom_on && exhausted && H.tier == 0u ? P.prom_min : 0u);
             }
             if (prom_on)
                 written += (uint32_t)__popcll(act & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
@@ -1848,7 +1833,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
                                                   L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
             D.section(1);
-            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : early_prom);
+            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
         } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
@@ -1859,7 +1844,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
                                                         RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
-            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : early_prom);
+            promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
         }
         D.section(2);
         if (prom_on)  // pixels written this iteration (promoted ones are counted by whoever finishes them)
