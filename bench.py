@@ -313,8 +313,9 @@ def launch_desc(n_spheres, spp, nparts, rng):
         pre = ("k_render<false,true> 2-spp exact-grid cost pre-pass (samples 0-1, resumed from"
                + ("; a pixel past 16 segments stops and restarts in the render)" if whole else ")"))
     return (f"rtx_render_rows launch = {pre} + k_cost_hist + k_heavy_split + k_cost_scatter + "
-            f"k_render<true> (cost-ordered persistent lanes, {scan}, heavy-pixel coop tiers, promotion)"
-            + (" [+ k_trace on the aux stream for a small or low share]" if not large and not whole else ""))
+            f"k_render<true> (cost-ordered persistent lanes at a wave priority from their projected remaining "
+            f"chains, {scan}, heavy-pixel coop tiers, promotion)"
+            + (" [+ k_trace on the aux stream for a row-split share]" if not large and not whole else ""))
 
 
 def build_provenance(rtx):
