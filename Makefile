@@ -56,14 +56,15 @@ clean:
 # product path):
 #   stress - candidate lists of 1 entry and coop resolve rounds of one scan
 #            step, so every overflow, round and fallback path runs all the
-#            time (tests/test_gpu_parity.py)
+#            time, and a 2 ms promotion valve (the heartbeat keeps live
+#            launches going) (tests/test_gpu_parity.py)
 #   prof   - per-section clock sums (tools/section_prof.py)
 #   ptime  - per-pixel start/end times (tools/pixel_timeline.py)
 #   cprof  - per-section clocks of tier-1 coop segments (tools/coop_prof.py)
 # Ad-hoc A/B builds for tools/variant_bench.py:
 #   make adhoc V=name VFLAGS="-DRTX_...=..."   -> lib/variants/librtx_name.so
 VARIANTS := stress prof ptime cprof
-VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=200000ull
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
@@ -74,7 +75,7 @@ variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
 $(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS)
 	mkdir -p $(VDIR)/$*
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$*/k.o
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -DRTX_SRC_SHA='"$(SRC_SHA)"' -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -DRTX_SRC_SHA='"$(SRC_SHA)"' -DRTX_VARIANT='"$*"' -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$*/h.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(VDIR)/$*/k.o $(VDIR)/$*/a.o $(VDIR)/$*/h.o
 
@@ -82,7 +83,7 @@ adhoc:
 	@test -n "$(V)" || (echo "usage: make adhoc V=name VFLAGS=..." && false)
 	mkdir -p $(VDIR)/$(V)
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$(V)/k.o
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_api.hip -o $(VDIR)/$(V)/a.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -DRTX_VARIANT='"$(V)"' -c $(SRC)/rtx_api.hip -o $(VDIR)/$(V)/a.o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/rtx_host.cpp -o $(VDIR)/$(V)/h.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $(VDIR)/librtx_$(V).so $(VDIR)/$(V)/k.o $(VDIR)/$(V)/a.o $(VDIR)/$(V)/h.o
 

@@ -24,6 +24,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -56,7 +57,11 @@ def parse():
                    help="rocprofv3 PMC child passes for HBM traffic (rank 0, N=1)")
     p.add_argument("--per-sample", type=int, default=1,
                    help="also time the per-sample-RNG kernel on the same frame (N=1, chain runs only)")
+    p.add_argument("--parts", default="2,4,8",
+                   help="N=1: time every part of these R-way row-tile splits on this device ('' = skip)")
     p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--probe-parts", type=int, default=0, help=argparse.SUPPRESS)  # --probe: an R-way split
+    p.add_argument("--probe-frames", type=int, default=1, help=argparse.SUPPRESS)  # --probe: whole frames
     return p.parse_args()
 
 
@@ -76,14 +81,39 @@ def probe(args):
     with rtx.Context(0) as ctx:
         ctx.upload_world(world)
         ctx.set_frame(frame)
-        ctx.render()
-        ctx.sync()
+        if args.probe_parts > 1:  # every part of an R-way row-tile split, once each
+            R, T = args.probe_parts, args.tile_rows
+            buf = ctx.alloc((rtx.part_rows(args.height, T, 0, R), args.width, 4))
+            for p in range(R):
+                ctx.render_rows(T, p, R, buf.ptr)
+            ctx.sync()
+            buf.free()
+        else:
+            for _ in range(max(1, args.probe_frames)):
+                ctx.render()
+            ctx.sync()
+
+
+def kernel_class(name):
+    """The role of one dispatch of an rtx_render_rows launch (rocprof
+    Kernel_Name), or None for the HIP runtime's own fills and copies."""
+    m = re.search(r"k_render<(true|false), (true|false), (true|false)>", name)
+    if m:
+        if m.group(2) == "true":
+            return "prepass"
+        return "render" if m.group(1) == "true" else "render_grid"
+    for k in ("k_render_ps", "k_trace", "k_cost_hist", "k_cost_scatter", "k_heavy_split", "k_unpermute",
+              "k_render_trivial", "k_deinterleave"):
+        if k in name:
+            return k
+    return None
 
 
 def _pmc_pass(args, counters, tag, rng=None):
     """One rocprofv3 --pmc pass over the --probe child (one frame through
-    the C-ABI). Returns {counter: summed value over the k_render dispatches},
-    or raises RuntimeError."""
+    the C-ABI). Returns {counter: summed value over the launch's rtx
+    dispatches, "by_kernel": {role: {counter: value}}}, or raises
+    RuntimeError."""
     exe = shutil.which("rocprofv3")
     if not exe:
         raise RuntimeError("rocprofv3 not found")
@@ -95,14 +125,22 @@ def _pmc_pass(args, counters, tag, rng=None):
     try:
         subprocess.run(cmd, check=True, capture_output=True, timeout=240)
         vals = {c: 0.0 for c in counters}
+        by = {}
         seen = set()
         for path in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
             for row in csv.DictReader(open(path)):
-                if "k_render" in row.get("Kernel_Name", "") and row.get("Counter_Name") in vals:
-                    vals[row["Counter_Name"]] += float(row["Counter_Value"])
-                    seen.add(row["Counter_Name"])
+                role = kernel_class(row.get("Kernel_Name", ""))
+                c = row.get("Counter_Name")
+                if role is None or c not in vals:
+                    continue
+                v = float(row["Counter_Value"])
+                vals[c] += v
+                by.setdefault(role, {k: 0.0 for k in counters})[c] += v
+                if role.startswith("render") or role == "k_render_ps":
+                    seen.add(c)
         if seen != set(counters):
-            raise RuntimeError(f"no k_render rows for {sorted(set(counters) - seen)}")
+            raise RuntimeError(f"no render rows for {sorted(set(counters) - seen)}")
+        vals["by_kernel"] = by
         return vals
     except subprocess.SubprocessError as e:
         raise RuntimeError(f"rocprofv3 {tag} failed: {type(e).__name__}") from e
@@ -114,15 +152,21 @@ def pmc_traffic(args):
     """HBM bytes per render launch from rocprofv3 PMC counters, per
     MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes
     (TCC slots), KB units, FETCH_SIZE x2 on gfx950 for wide coalesced reads.
-    Returns (bytes, details) or (None, reason)."""
+    Summed over every dispatch of the launch, and split per dispatch role
+    (pre-pass, sort, render, k_trace). Returns (bytes, details) or (None,
+    reason)."""
     try:
-        fetch = _pmc_pass(args, ["FETCH_SIZE"], "fetch")["FETCH_SIZE"]
-        write = _pmc_pass(args, ["WRITE_SIZE"], "write")["WRITE_SIZE"]
+        f = _pmc_pass(args, ["FETCH_SIZE"], "fetch")
+        w = _pmc_pass(args, ["WRITE_SIZE"], "write")
     except RuntimeError as e:
         return None, str(e)
+    fetch, write = f["FETCH_SIZE"], w["WRITE_SIZE"]
     kb = 2.0 * fetch + write
-    return kb * 1024.0, {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
-                         "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+    roles = sorted(set(f["by_kernel"]) | set(w["by_kernel"]))
+    split = {r: {"FETCH_SIZE_KB": round(f["by_kernel"].get(r, {}).get("FETCH_SIZE", 0.0), 1),
+                 "WRITE_SIZE_KB": round(w["by_kernel"].get(r, {}).get("WRITE_SIZE", 0.0), 1)} for r in roles}
+    return kb * 1024.0, {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "by_dispatch": split,
+                         "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024, every rtx dispatch of the launch"}
 
 
 SQ_COUNTERS = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU",
@@ -153,6 +197,8 @@ def pmc_valu(args, n_cu, launch_ms, rng=None):
         w = _pmc_pass(args, STALL_COUNTERS, "stall", rng)
     except RuntimeError as e:
         return {"skipped": str(e)}
+    v.pop("by_kernel", None)
+    w.pop("by_kernel", None)
     cycles = v["GRBM_GUI_ACTIVE"] / 8.0
     simds = 4 * n_cu
     # the FLOPS counters count per wave-instruction (FMA 2, ...): x64 lanes is
@@ -267,6 +313,57 @@ def cpu_baseline(args, world, frame, gpu_image, budget_s):
             "host": host_cpu()}, {"rows_checked": len(done), "values_differing": mism, "bit_exact": mism == 0}
 
 
+def part_scaling(ctx, args, world, frame, t1_ms, dev, parts=(2, 4, 8), frames=2, check_rows=8):
+    """The 1/2/4/8-GPU split rehearsed on this one device (N = 1 only): an
+    R-GPU frame gives rank p the rows rtx_render_rows(T, p, R) renders, so
+    timing every part of an R-way split here gives each rank's kernel time
+    and the critical path max_p t_p of the R-GPU frame (before its gather).
+    efficiency = t(1) / (R * max_p t_p), t(1) = the headline's launch time.
+    After timing, `check_rows` rows of each R's critical part are compared
+    bit for bit with the fp32 oracle (the checker, never the timed path)."""
+    import numpy as np
+    import torch
+    import rtx
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    W, H, T = args.width, args.height, args.tile_rows
+    threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16))
+    buf = torch.empty((rtx.part_rows(H, T, 0, 1), W, 4), dtype=torch.float32, device=dev)
+    out = {"t1_ms": round(t1_ms, 3), "frames_per_part": frames, "tile_rows": T,
+           "note": "each part of an R-way row-tile split timed on this one MI355X (HIP events around "
+                   "rtx_render_rows); critical_ms = max over parts; efficiency = t1 / (R * critical)"}
+    for R in parts:
+        times, segs = [], []
+        for p in range(R):
+            ctx.render_rows(T, p, R, buf.data_ptr())  # warm (and the schedule's buffers)
+            torch.cuda.synchronize()
+            ctx.stats_reset()
+            for _ in range(frames):
+                ctx.render_rows(T, p, R, buf.data_ptr())
+            torch.cuda.synchronize()
+            st = ctx.stats()
+            times.append(st.kernel_ms / max(1, st.launches))
+            segs.append(int(st.segments // max(1, st.launches)))
+        crit = max(times)
+        pc = times.index(crit)
+        # parity of the critical part: its last frame is not in buf any more
+        # unless it was the last part timed, so render it once more
+        ctx.render_rows(T, pc, R, buf.data_ptr())
+        torch.cuda.synchronize()
+        ids = rtx.part_row_ids(H, T, pc, R)
+        local = sorted(set(int(i) for i in np.linspace(0, len(ids) - 1, check_rows)))
+        got = buf[local].cpu().numpy()
+        want, _ = oracle.render_rows(world, frame, ids[local], nthreads=threads)
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        out[str(R)] = {"critical_ms": round(crit, 3), "efficiency": round(t1_ms / (R * crit), 4),
+                       "mean_ms": round(sum(times) / R, 3), "part_ms": [round(t, 3) for t in times],
+                       "part_segments": segs,
+                       "parity": {"part": pc, "rows_checked": len(local), "values_differing": int((~same).sum()),
+                                  "bit_exact": bool(same.all())}}
+    del buf
+    return out
+
+
 def per_sample_parity(world, frame, img, rows):
     """Checker for the per-sample line: a few rows of the per-sample frame
     against the fp32 oracle in the same RNG mode (bit for bit)."""
@@ -326,7 +423,8 @@ def build_provenance(rtx):
     info = rtx.build_info()
     tree = src_sha16(ROOT)
     return {"lib": os.path.relpath(rtx.LIB_PATH, ROOT), "lib_src_sha16": info.get("src_sha16"),
-            "tree_src_sha16": tree, "built_from_this_tree": info.get("src_sha16") == tree,
+            "tree_src_sha16": tree, "variant": info.get("variant", "product"),
+            "built_from_this_tree": info.get("src_sha16") == tree and info.get("variant", "product") == "product",
             "arch": info.get("arch")}
 
 
@@ -415,6 +513,12 @@ def main():
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
             cpu, parity = cpu_baseline(args, world, frame, host_img, args.cpu_seconds)
+        # the 1/2/4/8-GPU split rehearsed on this device (BASELINE.json metric:
+        # "1/2/4/8-GPU scaling"); the real N-GPU runs are the driver's
+        parts = None
+        if R == 1 and args.parts:
+            parts = part_scaling(ctx, args, world, frame, launch_ms, dev,
+                                 parts=[int(x) for x in args.parts.split(",") if x])
         # The north star's kernel shape — one lane per (pixel, sample) — on the
         # same frame with per-(pixel, sample) seeds (rtx_frame.rng_mode 1,
         # DESIGN.md §3a): reported beside the headline, which stays the
@@ -473,8 +577,14 @@ def main():
             "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(alg_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
+                             "achieved_kind": "algorithmic bytes (framebuffer + scene) / launch time",
                              "algorithmic_bytes_per_launch": alg_bytes,
-                             "traffic": None if traffic is None else round(traffic)},
+                             "traffic": None if traffic is None else round(traffic),
+                             "measured": None if traffic is None else round(traffic / (launch_ms * 1e-3) / 1e9, 3),
+                             "measured_frac": None if traffic is None
+                             else round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                             "measured_kind": "rocprofv3 PMC traffic per launch / launch time"},
+            "part_scaling": parts,
             "cpu_baseline": cpu,
             "parity": parity,
             "per_sample_rng": per_sample,

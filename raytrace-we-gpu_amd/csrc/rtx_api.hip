@@ -178,7 +178,13 @@ int rtx_version(void) { return RTX_VERSION; }
 // (Makefile SRC_SHA: sha256 over csrc/* and include/rtx.h, first 16 hex
 // digits) and the offload target, so a run can show that the library it
 // loaded is the one its tree's sources build.
-const char *rtx_build_info(void) { return "src_sha16=" RTX_SRC_SHA " arch=gfx950"; }
+// A variant build (Makefile variants/adhoc, tools/build_commit_variant.sh:
+// other compile-time choices from the same sources) also names itself, so
+// it is never mistaken for the product library.
+#ifndef RTX_VARIANT
+#define RTX_VARIANT "product"
+#endif
+const char *rtx_build_info(void) { return "src_sha16=" RTX_SRC_SHA " arch=gfx950 variant=" RTX_VARIANT; }
 
 const char *rtx_last_error(void) { return g_last_error.c_str(); }
 

@@ -15,7 +15,8 @@
 // depth 50, random_world with 326 spheres, camera (13,2,3) -> 0, vfov 20,
 // aspect 16/9 (DxCSApp.cpp:133,176-179,330-331) — uploaded as the reference's
 // own WorldDef and PerFrame cbuffer bytes through rtx_world_from_worlddef /
-// rtx_frame_from_perframe (later options still override).
+// rtx_frame_from_perframe; a preset: every other option, before or after
+// it, overrides its values.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +42,14 @@ int main(int argc, char **argv) {
     cfg.spp = 100;
     cfg.depth = 50;
     cfg.grid_half_extent = 11;
+    // --reference-frame is a preset: it sets the reference's values first,
+    // wherever it stands, and every other option then overrides them
+    for (int i = 1; i < argc; ++i) {
+        if (std::string(argv[i]) == "--reference-frame") {
+            cfg = rtx::AppConfig();  // the reference's values (include/rtx_app.hpp)
+            cfg.cbuffers = true;
+        }
+    }
     int frames = 1, device = 0;
     bool accumulate = false;
     std::string pfm, ppm;
@@ -66,8 +75,7 @@ int main(int argc, char **argv) {
         else if (a == "--accumulate") accumulate = true;
         else if (a == "--lambert-guard") cfg.lambert_guard = true;
         else if (a == "--reference-frame") {
-            cfg = rtx::AppConfig();  // the reference's values (include/rtx_app.hpp)
-            cfg.cbuffers = true;
+            // a preset, applied before the loop (below): here it only keeps its place
         }
         else if (a == "--rng") {
             const std::string m = next();

@@ -79,7 +79,8 @@ struct KParams {
     // wave hands a pixel whose projected remaining segments exceed prom_min
     // to k_trace at a sample boundary (rtx_kernels.hip, promote)
     uint32_t *prom;                // [0] entries claimed [1] entries taken [2] k_render-owned pixels written
-                                   // [3] k_render has started (set by its workgroup 0); NULL: off
+                                   // [3] k_render has started (set by its workgroup 0)
+                                   // [4] heartbeat: s_memrealtime >> 10 of a tracing wave (valve); NULL: off
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
@@ -113,7 +114,7 @@ struct KTune {
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
     double prom_big;                                           // ... for scenes without the coop's LDS copy
-    uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2, 4, 8)
+    uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2 or 4)
     double trace_solo;                                         // ... one per wave above this x share (k0)
     uint32_t cap_split;                                        // pre-pass cap of a row-split part (0: none)
     double dyn1, dyn2, dyn3;  // lane-mode wave priority 1/2/3 above these x the mean pixel (dyn1 0: static hot slots)

@@ -117,7 +117,7 @@ constexpr double kPromSmall = 400.0, kPromLow = 300.0, kPromMedium = 400.0, kPro
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
-// k_trace: tier-1 pixels per wave (1, 2, 4, 8), and the key bar (x share)
+// k_trace: tier-1 pixels per wave (1, 2 or 4: rtx_set_schedule), and the key bar (x share)
 // above which a pixel is traced alone in its wave nonetheless
 constexpr uint32_t kTraceGroup = 4;
 constexpr double kTraceSolo = 6.0;
@@ -1639,9 +1639,30 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
 // server that sees no pixel written for kPromValveTicks leaves and flags the
 // launch (KParams::errors: rtx_sync / rtx_get_stats report it), so a bug shows
 // as an error, never as a hung GPU or a silently unwritten pixel.
-constexpr unsigned long long kPromValveTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+// Progress is a pixel written (prom[2]) or a heartbeat: every wave still
+// tracing once its queue is exhausted (k_render) and every k_trace wave
+// stores the time into prom[4] at most every kBeatTicks (beat), so a long
+// but live chain — a big scene, a high spp — never trips the valve however
+// long it runs without another pixel finishing; only a launch in
+// which nothing traces any more does. The stress build (make all) runs with
+// a 2 ms valve, so its GPU tests exercise exactly that.
+#ifndef RTX_PROM_VALVE_TICKS
+#define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s of s_memrealtime (100 MHz)
+#endif
+constexpr unsigned long long kPromValveTicks = RTX_PROM_VALVE_TICKS;
+constexpr unsigned long long kBeatTicks = kPromValveTicks / 16u;
+constexpr uint32_t kBeatShift = 10;  // prom[4] holds s_memrealtime >> 10 (10.24 us units, wraps every ~12 h)
 __device__ __forceinline__ void flag_error(const KParams &P, uint32_t bit) {
     if (P.errors && (threadIdx.x & 63u) == 0u) atomicOr(P.errors, bit);
+}
+// The heartbeat (wave-uniform; `last` is the wave's previous beat).
+__device__ __forceinline__ void beat(const KParams &P, unsigned long long &last) {
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (now - last > kBeatTicks) {
+        last = now;
+        if ((threadIdx.x & 63u) == 0u)
+            __hip_atomic_store(&P.prom[4], (uint32_t)(now >> kBeatShift), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, uint32_t npix, uint32_t target,
                                               bool helper, Lane &W) {
@@ -1651,12 +1672,15 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
     auto ld = [](const uint32_t *p) {
         return (uint32_t)__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     };
+    uint32_t seen_beat = 0;
     for (;;) {
         const uint32_t done = ld(&P.prom[2]);
         if (done >= target) return false;
         if (helper && ld(&P.prom[3]) == 0u) return false;  // k_render has not started: it serves itself
-        if (done != seen) {  // progress: the valve restarts
+        const uint32_t bt = ld(&P.prom[4]);
+        if (done != seen || bt != seen_beat) {  // progress (a pixel written, or a heartbeat): the valve restarts
             seen = done;
+            seen_beat = bt;
             t0 = __builtin_amdgcn_s_memrealtime();
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1761,6 +1785,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
     // promotion's exit count: the pixels this kernel owns (tier 1 is k_trace's when it runs beside it)
     const uint32_t owned = npix - (P.trace_ext != 0u ? H.k1 : 0u);
     uint32_t written = 0;  // pixels this wave wrote since it last reported
+    unsigned long long last_beat = 0;  // the wave's last heartbeat (beat)
     Diag D;
     D.begin();
     for (;;) {
@@ -1779,12 +1804,18 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             if ((threadIdx.x & 63u) == 0u) srv = atomicCAS(&s_server, 0u, threadIdx.x / 64u + 1u);
             srv = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)srv, 0, 64));
             if (srv != 0u && srv != threadIdx.x / 64u + 1u) break;  // another wave serves this block
-            if (!take_promoted(P, F, npix, owned, false, L)) break;
+            if (!take_promoted(P, F, npix, owned, false, L)) {
+                // leaving: free the block's server slot, so that a wave of
+                // this block that goes idle later can serve in its place
+                if ((threadIdx.x & 63u) == 0u) atomicExch(&s_server, 0u);
+                break;
+            }
             L.active = (threadIdx.x & 63u) == 0u;  // one ray, traced by the whole wave (tier-1 coop)
             H.tier = 1;
             continue;
         }
         const uint64_t was_active = act;
+        if (prom_on && (exhausted || H.tier != 0u)) beat(P, last_beat);  // still tracing: the valve sees progress
         D.iteration(act);
         if (heavy || (exhausted && (uint32_t)__popcll(act) <= P.coop_max)) {
             D.tail_iteration();
@@ -1874,15 +1905,17 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
         return (uint32_t)__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     };
     unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t seen = ~0u;
+    uint32_t seen = ~0u, seen_beat = 0;
     const uint32_t nneed = (uint32_t)__popcll(need);
     // this lane's group among the idle ones (only meaningful in idle groups)
     const uint32_t rank = (uint32_t)__popcll(need & ((1ull << (lane & ~((1u << lg) - 1u))) - 1ull));
     for (;;) {
         const uint32_t done = ld(&P.prom[2]);
         if (done >= target || ld(&P.prom[3]) == 0u) return -1;
-        if (done != seen) {
+        const uint32_t bt = ld(&P.prom[4]);
+        if (done != seen || bt != seen_beat) {  // progress: a pixel written or a heartbeat
             seen = done;
+            seen_beat = bt;
             t0 = __builtin_amdgcn_s_memrealtime();
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1976,6 +2009,7 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     uint32_t segs = 0;  // segments traced, counted by the first lane of each group
     bool t1_done = k1 == 0u;
     bool serve_done = P.prom == nullptr;
+    unsigned long long last_beat = 0;  // the wave's last heartbeat (beat)
     for (;;) {
         uint64_t act = __ballot(W.active);
         if (act == 0ull && t1_done) lg = lg_many;  // an idle wave serves promotions in groups again
@@ -2035,9 +2069,11 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             do {
                 trace_group_segment<6>(P, F, sl, W, ended);
                 ++n;
+                if (P.prom) beat(P, last_beat);
             } while (!ended);
             if (first) segs += n;
         } else {
+            if (P.prom) beat(P, last_beat);
             if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 (rtx_set_schedule)
                 trace_group_segment<5>(P, F, sl, W, ended);
             else

@@ -266,11 +266,13 @@ def part_row_ids(height: int, tile_rows: int, part: int, nparts: int) -> np.ndar
 
 def _require_schedule_abi(lib: C.CDLL):
     """rtx_schedule grew in 1.2.0 (promote_big_scene, refill_chunk), 1.3.0
-    (trace_solo_bar, trace_group) and 1.4.0 (prio_bar1..3): an older library
-    would read this module's struct at the wrong offsets."""
+    (trace_solo_bar, trace_group) and 1.4.0 (prio_bar1..3): a library of
+    another major.minor (older or newer) would read this module's struct at
+    the wrong offsets, so it must match exactly (patch levels may differ)."""
     v = int(lib.rtx_version())
-    if v < SCHEDULE_ABI or not hasattr(lib, "rtx_set_schedule"):
-        raise RtxError(f"library ABI {v} predates the rtx_schedule layout {SCHEDULE_ABI} this binding passes")
+    if v // 10 != SCHEDULE_ABI // 10 or not hasattr(lib, "rtx_set_schedule"):
+        raise RtxError(f"library ABI {v} does not match the rtx_schedule layout {SCHEDULE_ABI} this binding "
+                       "passes (major.minor must be equal)")
 
 
 def schedule_defaults() -> rtx_schedule:

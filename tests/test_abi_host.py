@@ -158,19 +158,25 @@ def test_ctypes_mirror_matches_header_layout(rtx, tmp_path):
             assert got[(name, field)] == getattr(cls, field).offset, (name, field)
 
 
-def test_schedule_calls_refuse_an_older_abi(rtx):
-    """rtx_schedule grew in ABI 1.2.0: the binding refuses to pass its layout to
-    a library that reports an older version (it would read the fields after
-    promote_large at the wrong offsets) instead of installing a wrong schedule."""
-    class OldLib:
+def test_schedule_calls_refuse_another_abi(rtx):
+    """rtx_schedule grew in ABI 1.2.0, 1.3.0 and 1.4.0: the binding refuses to
+    pass its layout to a library of another major.minor, older or newer (it
+    would read the fields at the wrong offsets), instead of installing a
+    wrong schedule; a different patch level is accepted."""
+    class Lib:
+        def __init__(self, v):
+            self.v = v
+
         def rtx_version(self):
-            return 130
+            return self.v
 
         def rtx_set_schedule(self, *a):
             raise AssertionError("must not be called")
 
-    with pytest.raises(rtx.RtxError, match="predates"):
-        rtx._require_schedule_abi(OldLib())
+    for v in (130, 150, 200):
+        with pytest.raises(rtx.RtxError, match="does not match"):
+            rtx._require_schedule_abi(Lib(v))
+    rtx._require_schedule_abi(Lib(rtx.SCHEDULE_ABI + 1))  # a patch level
     rtx._require_schedule_abi(rtx.load_library())  # the in-tree library passes
 
 
@@ -183,3 +189,4 @@ def test_library_built_from_this_tree(rtx):
     info = rtx.build_info()
     assert info.get("arch") == "gfx950"
     assert info.get("src_sha16") == src_sha16(), "librtx.so is stale: rebuild (make)"
+    assert info.get("variant") == "product", info

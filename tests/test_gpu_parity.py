@@ -889,7 +889,8 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
     ctx.set_schedule()
 
 
-def test_promotion_across_the_chip(gpu_ctx, oracle, rtx):
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+def test_promotion_across_the_chip(request, oracle, rtx, ctx_name):
     """Promotion with every workgroup of the chip taking part: a
     1280x720 frame (2.8 pixels per resident lane: a "medium" part) with
     promote_* 1 — nearly every pixel still in flight once the queue is empty
@@ -898,7 +899,11 @@ def test_promotion_across_the_chip(gpu_ctx, oracle, rtx):
     kernels running together). Entries cross XCDs (the queue is one array;
     producers and servers sit on all 8). The launch must complete (no
     RTX_ERR_INCOMPLETE from rtx_get_stats), rows bit-exact, and the segment
-    count equal to an independent exact-grid pass's."""
+    count equal to an independent exact-grid pass's. Through the stress build
+    the promotion valve is 2 ms: the frame's last chains run
+    longer than that without another pixel finishing, so the launch
+    completes only if the tracing waves' heartbeat counts as progress."""
+    gpu_ctx = request.getfixturevalue(ctx_name)
     W, H, T = 1280, 720, 5
     world = rtx.random_world(11, depth=50, spp=12)
     frame = rtx.camera_look_at(W, H, aspect=W / H)

@@ -1,9 +1,13 @@
 #!/bin/bash
-# One GPU-box session: every GPU step under its own timeout; a crash,
-# abort, or timeout (exit >= 124 or signal) ends the script there. Test
-# failures (exit 1/2: pytest failures, Python exceptions) do not stop the
-# later measurement steps.
-# Usage: tools/gpu_session.sh TAG [steps...]   steps: ubench tests smoke bench prof pmc
+# The one GPU-box session runner: every GPU step under its own timeout; a
+# crash, abort, or timeout (exit >= 124 or signal) ends the script there.
+# Test failures (exit 1/2: pytest failures, Python exceptions) do not stop
+# the later measurement steps. Steps are named on the command line and
+# parameterised through environment variables (below), so a session is one
+# line, e.g.
+#   tools/gpu_session.sh R7a tests smoke bench prof prof8 c5b
+#   PTLIB=ptime PTPARTS="4 8" HSETS='--sets "default;pb1=0"' tools/gpu_session.sh R7b ptime hsweep
+# Usage: tools/gpu_session.sh TAG [steps...]   (default: ubench tests smoke bench prof)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}; shift
@@ -30,20 +34,26 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-                python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off ;;
-    c3b)    run c3b 900 python bench.py --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 ;;
-    c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --per-sample ${C5PS:-0} ;;
-    c3ps)   run c3ps 900 python bench.py --rng per-sample --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 ;;
-    c5ps)   run c5ps 900 python bench.py --rng per-sample --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 ;;
+                python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off --parts '' --per-sample 0 ;;
+    prof8)  run prof8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof8" -o run -- \
+                python3 bench.py --probe --probe-parts 8 ;;
+    psprof) run psprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/psprof" -o run -- \
+                python3 bench.py --probe --rng per-sample --probe-frames 3 ;;
+    gtest)  run gtest 600 python -u -m pytest ${GTESTS:-tests/test_gpu_parity.py} -m gpu -x -q --timeout 120 \
+                --timeout-method thread ;;
+    c3b)    run c3b 900 python bench.py --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 --parts '' ;;
+    c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --parts '' --per-sample ${C5PS:-0} ;;
+    c3ps)   run c3ps 900 python bench.py --rng per-sample --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 --parts '' ;;
+    c5ps)   run c5ps 900 python bench.py --rng per-sample --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --parts '' ;;
     variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ${VARGS:-} ${VNAMES:-} ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
-    c2ps)   run c2ps 600 python bench.py --rng per-sample --steps 5 --warmup 1 --cpu-seconds 10 ;;
+    c2ps)   run c2ps 600 python bench.py --rng per-sample --steps 5 --warmup 1 --cpu-seconds 10 --parts '' ;;
     timeline) run timeline 300 python tools/wave_timeline.py ;;
     vtimeline) for v in ${VTL:-blk64 lpt lpt_blk64}; do
               run timeline_$v 300 python tools/wave_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_$v.so; done ;;
     sprof)  run sprof 300 python tools/section_prof.py raytrace-we-gpu_amd/lib/variants/librtx_prof.so ;;
-    parts)  run parts 600 python tools/part_scaling.py ${PLIBS:-} ;;
-    hsweep) run hsweep 900 python tools/heavy_sweep.py --parts ${HPARTS:-8} --rounds ${HROUNDS:-2} ${HSETS:-} ;;
+    parts)  run parts 600 python tools/part_scaling.py ${PARGS:-} ${PLIBS:-} ;;
+    hsweep) eval run hsweep 900 python tools/heavy_sweep.py --parts ${HPARTS:-8} --rounds ${HROUNDS:-2} ${HSETS:-} ;;
     psparts) run psparts 600 python tools/part_scaling.py --rng per-sample ;;
     cprof)  run cprof 300 python tools/coop_prof.py raytrace-we-gpu_amd/lib/variants/librtx_cprof.so ;;
     ptime)  run ptime 600 python tools/pixel_timeline.py raytrace-we-gpu_amd/lib/variants/librtx_${PTLIB:-ptime}.so \
