@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--probe-parts", type=int, default=0, help=argparse.SUPPRESS)  # --probe: an R-way split
     p.add_argument("--probe-frames", type=int, default=1, help=argparse.SUPPRESS)  # --probe: whole frames
+    p.add_argument("--probe-scan", type=int, default=0, help=argparse.SUPPRESS)  # --probe: scan-rate reps
     return p.parse_args()
 
 
@@ -81,7 +82,9 @@ def probe(args):
     with rtx.Context(0) as ctx:
         ctx.upload_world(world)
         ctx.set_frame(frame)
-        if args.probe_parts > 1:  # every part of an R-way row-tile split, once each
+        if args.probe_scan:  # hit_world alone at the render's occupancy (rtx_debug_scan_rate)
+            ctx.debug_scan_rate(args.probe_scan)
+        elif args.probe_parts > 1:  # every part of an R-way row-tile split, once each
             R, T = args.probe_parts, args.tile_rows
             buf = ctx.alloc((rtx.part_rows(args.height, T, 0, R), args.width, 4))
             for p in range(R):
@@ -103,13 +106,13 @@ def kernel_class(name):
             return "prepass"
         return "render" if m.group(1) == "true" else "render_grid"
     for k in ("k_render_ps", "k_trace", "k_cost_hist", "k_cost_scatter", "k_heavy_split", "k_unpermute",
-              "k_render_trivial", "k_deinterleave"):
+              "k_render_trivial", "k_deinterleave", "k_debug_scan_rate"):
         if k in name:
             return k
     return None
 
 
-def _pmc_pass(args, counters, tag, rng=None):
+def _pmc_pass(args, counters, tag, rng=None, extra=()):
     """One rocprofv3 --pmc pass over the --probe child (one frame through
     the C-ABI). Returns {counter: summed value over the launch's rtx
     dispatches, "by_kernel": {role: {counter: value}}}, or raises
@@ -119,7 +122,7 @@ def _pmc_pass(args, counters, tag, rng=None):
         raise RuntimeError("rocprofv3 not found")
     base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
             "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
-            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", rng or args.rng]
+            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", rng or args.rng] + list(extra)
     out = tempfile.mkdtemp(prefix=f"rtx_pmc_{tag}_")
     cmd = [exe, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
     try:
@@ -136,7 +139,7 @@ def _pmc_pass(args, counters, tag, rng=None):
                 v = float(row["Counter_Value"])
                 vals[c] += v
                 by.setdefault(role, {k: 0.0 for k in counters})[c] += v
-                if role.startswith("render") or role == "k_render_ps":
+                if role.startswith("render") or role in ("k_render_ps", "k_debug_scan_rate"):
                     seen.add(c)
         if seen != set(counters):
             raise RuntimeError(f"no render rows for {sorted(set(counters) - seen)}")
@@ -237,6 +240,41 @@ def pmc_valu(args, n_cu, launch_ms, rng=None):
                        "SQ_ACTIVE_INST_* / SQ_WAIT_INST_ANY (ready, not issued) / SQ_WAIT_ANY (s_waitcnt, "
                        "barrier) over SQ_WAVE_CYCLES (its own pass)",
             "counters": v, "stall_counters": w, "cus": n_cu}
+
+
+SCAN_REPS = 200
+
+
+def issue_ceiling(args, ctx, executed, n_cu):
+    """The VALU issue rate hit_world's own instruction mix sustains at the
+    render's occupancy: rtx_debug_scan_rate runs the
+    render's lane-mode hit_world (prefiltered scan + resolve) and nothing
+    else on a full-occupancy grid of the render's shape; one rocprofv3 pass
+    over that launch gives its VALU instructions per SIMD-cycle. The render's
+    rate over the same measure says how close the whole kernel (scan, resolve,
+    shading, scheduling) runs to that ceiling. Small scenes (<= 640 spheres)."""
+    if not executed or "counters" not in executed:
+        return {"skipped": "needs the N=1 PMC passes"}
+    ms, wave_segs = ctx.debug_scan_rate(SCAN_REPS)  # (a warm run; the profiled one is the --probe child's)
+    try:
+        v = _pmc_pass(args, ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"], "scan",
+                      extra=["--probe-scan", str(SCAN_REPS)])
+    except RuntimeError as e:
+        return {"skipped": str(e)}
+    simds = 4 * n_cu
+    probe_ipc = v["SQ_INSTS_VALU"] / (simds * v["GRBM_GUI_ACTIVE"] / 8.0)
+    rc = executed["counters"]
+    render_ipc = rc["SQ_INSTS_VALU"] / (simds * rc["GRBM_GUI_ACTIVE"] / 8.0)
+    return {"probe": "rtx_debug_scan_rate: the render's lane-mode hit_world alone, full occupancy, "
+                     f"{SCAN_REPS} reps of one primary ray per lane",
+            "probe_ms": round(ms, 3), "probe_wave_segments": wave_segs,
+            "probe_valu_per_wave_segment": round(v["SQ_INSTS_VALU"] / max(1, wave_segs), 1),
+            "probe_valu_per_simd_cycle": round(probe_ipc, 4),
+            "probe_cycles_per_valu": round(1.0 / probe_ipc, 3) if probe_ipc else None,
+            "render_valu_per_simd_cycle": round(render_ipc, 4),
+            "render_cycles_per_valu": round(1.0 / render_ipc, 3) if render_ipc else None,
+            "render_frac_of_ceiling": round(render_ipc / probe_ipc, 4) if probe_ipc else None,
+            "counters": {k: v[k] for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE")}}
 
 
 def roofline_of(executed, launch_ms, tests_per_launch):
@@ -506,9 +544,12 @@ def main():
         alg_bytes = rows0 * W * 16 + world.count * 32  # framebuffer + scene
         n_cu = torch.cuda.get_device_properties(local_rank).multi_processor_count
         traffic, pmc_note, executed = (None, "skipped (PMC passes run at N=1 with --pmc auto)", None)
+        ceiling = None
         if args.pmc == "auto" and R == 1:
             traffic, pmc_note = pmc_traffic(args)
             executed = pmc_valu(args, n_cu, launch_ms)
+            if world.count <= 640 and args.rng == "chain":
+                ceiling = issue_ceiling(args, ctx, executed, n_cu)
         host_img = image.cpu().numpy() if R == 1 else None
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
@@ -554,7 +595,7 @@ def main():
                     kernel=launch_desc(world.count, args.spp, R, args.rng), kernel_ms=round(launch_ms, 4),
                     sphere_tests_per_launch=tests_per_launch,
                     segments_per_sample=round(st.segments / max(1, st.samples), 4),
-                    pmc=pmc_note, executed=executed)
+                    pmc=pmc_note, executed=executed, issue_ceiling=ceiling)
         line = {
             "metric": "Msamples/sec (pixels x spp) at 1920x1080 spp=100 depth=50",
             "value": round(value, 3),

@@ -38,8 +38,9 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 140 /* 1.4.0 */
+#define RTX_VERSION 141 /* 1.4.1 */
 /* ABI notes.
+ *  1.4.1: rtx_debug_scan_rate (a diagnostic; no layout change).
  *  1.4.0: rtx_schedule.prio_bar1..3 (after prepass_cap_split, before
  *         `reserved`): dynamic lane-mode wave priority; the struct grew by
  *         12 bytes.
@@ -423,6 +424,17 @@ RTX_API int rtx_debug_wave_times(rtx_ctx *ctx, size_t max_waves, unsigned long l
  * (width * height uint32, row 0 = image bottom). Does not touch the
  * framebuffer or the stats. Synchronous. */
 RTX_API int rtx_debug_pixel_cost(rtx_ctx *ctx, uint32_t spp, uint32_t *host_cost);
+/* Issue-rate probe of hit_world's instruction mix (ABI 1.4.1): a
+ * full-occupancy grid shaped like the render (same workgroups, register
+ * budget and LDS) in which every lane runs the render's lane-mode hit_world
+ * (prefiltered scan + resolve, ShaderCompute.hlsl:188-205) `reps` times on
+ * one primary ray of the current frame, and nothing else. *ms: the launch's
+ * HIP-event time; *wave_segments: waves x reps (one wave-segment = 64 ray
+ * segments' hit_world). A profiler's SQ_INSTS_VALU over this launch gives
+ * the VALU issue rate the scan-and-resolve mix sustains on its own — the
+ * ceiling for the render's hit_world section. Scenes up to 640 spheres (the
+ * render's LDS-copy scenes); needs a world and a frame. Synchronous. */
+RTX_API int rtx_debug_scan_rate(rtx_ctx *ctx, uint32_t reps, float *ms, unsigned long long *wave_segments);
 
 #ifdef __cplusplus
 }

@@ -954,6 +954,35 @@ int rtx_debug_hit_world(rtx_ctx *c, const float *rays, uint32_t nrays, float t_m
     return rtx_debug_hit_world_from(c, rays, nrays, t_min, t_max, 0, out);
 }
 
+int rtx_debug_scan_rate(rtx_ctx *c, uint32_t reps, float *ms, unsigned long long *wave_segments) {
+    if (!c || !ms || !wave_segments) return fail(RTX_ERR_INVALID, "rtx_debug_scan_rate: null argument");
+    if (!c->have_world) return fail(RTX_ERR_STATE, "rtx_debug_scan_rate: no world uploaded");
+    if (!c->have_frame) return fail(RTX_ERR_STATE, "rtx_debug_scan_rate: no frame set");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const rtx_frame &f = c->frame;
+    rtx::KParams p = make_params(c, f.height, 1, 0, 1, nullptr, nullptr, 0, f.frame_index);
+    unsigned long long *sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    uint32_t waves = 0;
+    RTX_HIP(hipMalloc(&sink, sizeof(unsigned long long)));
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMemsetAsync(sink, 0, sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
+    if (e == hipSuccess) e = rtx::launch_debug_scan_rate(p, reps, sink, &waves, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(sink);
+    if (e == hipErrorInvalidValue) return fail(RTX_ERR_INVALID, "rtx_debug_scan_rate: scenes up to 640 spheres");
+    if (e != hipSuccess) return hip_fail(e, "rtx_debug_scan_rate");
+    *wave_segments = (unsigned long long)waves * reps;
+    return RTX_OK;
+}
+
 int rtx_debug_math(rtx_ctx *c, int fn, const float *in0, const float *in1, uint32_t n, float *out) {
     if (!c || (n && (!in0 || !out))) return fail(RTX_ERR_INVALID, "rtx_debug_math: null argument");
     if (fn < RTX_FN_SQRT || fn > RTX_FN_LAMBERT_DIR_GUARD)

@@ -68,6 +68,8 @@ struct KParams {
     uint32_t cost_spp;             // samples the pre-pass traced (the render resumes after them)
     uint32_t cost_cap;             // pre-pass: a pixel still tracing after this many segments stops (0: none)
     uint32_t cost_capped;          // ... and records this cost
+    uint32_t *pre_done;            // persistent pre-pass: pixels finished (NULL: no early stop)
+    uint32_t pre_stop;             // ... it stops its pixels once at most this many are in flight
     float4 *state;                 // per pixel (acc, seed) after cost_spp samples: written by the
                                    // pre-pass, resumed from by the persistent render (NULL = none)
     uint32_t prio_slots;           // normal-queue slots whose waves run at top priority
@@ -139,7 +141,8 @@ struct KSchedule {
 };
 constexpr uint32_t kCostBuckets = 256;
 // Scheduling words after the two bucket arrays (counts, cursors), zeroed per
-// launch: heavy[8] (KParams::heavy), then prom[8] (KParams::prom).
+// launch: heavy[8] (KParams::heavy; heavy[6]: the pre-pass's pre_done), then
+// prom[8] (KParams::prom).
 constexpr uint32_t kSchedWords = 16;
 #ifndef RTX_COST_SPP
 #define RTX_COST_SPP 2
@@ -162,6 +165,9 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
                                uint32_t max_rows, hipStream_t stream);
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays,
                                   float t_min, float t_max, uint32_t start_block, float *out,
+                                  hipStream_t stream);
+// hit_world alone at the render's occupancy (rtx_debug_scan_rate); *waves: the grid's waves
+hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
                                   hipStream_t stream);
 hipError_t launch_debug_math(int fn, const float *in0, const float *in1, uint32_t n,
                              float *out, hipStream_t stream);

@@ -47,23 +47,55 @@ namespace {
 
 constexpr float kTMin = 0.001f;  // hit_world(cur_ray, 0.001, 1.#INF, h), :262
 
-struct Frame {
+struct FrameVals {
     f3 org, hor, ver, llc;
     float img_w, img_h;
     f3 lu, lv;
     float lens_r;
 };
+// The frame constants (camera, image size, lens: the PerFrame cbuffer's
+// values) are read where a sample starts, straight from the launch's kernel
+// arguments (scalar loads through an opaque kernarg pointer), not held for
+// the whole kernel: held, their 21 SGPRs were spilled to VGPR lanes and
+// every sample start paid ~18 v_readlane restores in VALU issue slots.
+// Every kernel that starts samples takes `const KParams` as its only
+// argument, so the kernarg segment begins with it.
+struct Frame {};
+typedef const __attribute__((address_space(4))) KParams *kparams_cp;
+__device__ __forceinline__ FrameVals frame_vals() {
+    // opaque (reloaded at each use, never hoisted into live SGPRs): passed
+    // through a VGPR by an empty asm (an SGPR-constrained asm in divergent
+    // code does not compile), then made uniform again by readfirstlane
+    const uint64_t a = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    kparams_cp kp = (kparams_cp)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    FrameVals F;
+    F.org = mk3(kp->org[0], kp->org[1], kp->org[2]);
+    F.hor = mk3(kp->hor[0], kp->hor[1], kp->hor[2]);
+    F.ver = mk3(kp->ver[0], kp->ver[1], kp->ver[2]);
+    F.llc = mk3(kp->llc[0], kp->llc[1], kp->llc[2]);
+    F.img_w = kp->img_w;
+    F.img_h = kp->img_h;
+    F.lu = mk3(kp->lens_u[0], kp->lens_u[1], kp->lens_u[2]);
+    F.lv = mk3(kp->lens_v[0], kp->lens_v[1], kp->lens_v[2]);
+    F.lens_r = kp->lens_r;
+    return F;
+}
 
 // get_ray (ShaderCompute.hlsl:118-127): dir = llc + s*H + t*V - origin.
-__device__ __forceinline__ void get_ray(const Frame &F, float s, float t, f3 &o, f3 &d) {
+__device__ __forceinline__ void get_ray(const FrameVals &F, float s, float t, f3 &o, f3 &d) {
     o = F.org;
     d = ((F.llc + s * F.hor) + t * F.ver) - F.org;
 }
 
 // CSMain's per-sample jitter (ShaderCompute.hlsl:306-307): two hash2 calls,
 // u takes .x of the first, v takes .y of the second.
-__device__ __forceinline__ void start_sample(const Frame &F, uint32_t x, uint32_t y, float &seed,
+__device__ __forceinline__ void start_sample(const Frame &, uint32_t x, uint32_t y, float &seed,
                                              f3 &o, f3 &d) {
+    const FrameVals F = frame_vals();
     float h0, h1, g0, g1;
     hash2(seed, h0, h1);
     const float u = ((float)x + h0 * 1.1f) / (F.img_w - 1.0f);
@@ -141,6 +173,12 @@ constexpr double kDynPrio1 = 0.5, kDynPrio2 = 1.0, kDynPrio3 = 1.5;
 #define RTX_COST_CAP_LARGE 24  // C5 1,672 -> 1,623 ms (12: 1,659; the cap as the cost: 12 1,666, 6 1,952; R4g, R4h)
 #endif
 constexpr uint32_t kCostCap = RTX_COST_CAP, kCostCapLarge = RTX_COST_CAP_LARGE;
+// The persistent (large-scene) pre-pass stops once at most this fraction of
+// its lanes still hold a pixel (pre_stop; 0: runs to the end)
+#ifndef RTX_PRE_STOP
+#define RTX_PRE_STOP 0.25
+#endif
+constexpr double kPreStopFrac = RTX_PRE_STOP;
 constexpr uint32_t kPrioFracX100 = 20;  // hot-wave priority: prio_slots = this % of the resident lanes
 constexpr int kTailPrio = 1;            // wave priority of a normal wave in its coop tail
 constexpr uint32_t kRB = 256;           // threads per render workgroup
@@ -150,6 +188,15 @@ constexpr uint32_t kRB = 256;           // threads per render workgroup
                               // dwords to scratch) sit in per-segment and coop code, none in the scan loop
 #endif
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
+// The large-scene chain kernels (kPF: candidate lists of RTX_CAND_PF entries
+// and a 1-KiB scan tile per wave, ~34 KB of LDS per workgroup) fit 4
+// workgroups per CU's 160 KB of LDS, i.e. 4 waves per SIMD whatever their
+// registers allow: compiled for 5 they spilled 134 VGPRs (200 B/lane of
+// scratch) and 180 SGPRs for occupancy they never get; for 4 they have 128.
+#ifndef RTX_WAVES_PER_SIMD_PF
+#define RTX_WAVES_PER_SIMD_PF 4
+#endif
+#define RTX_RENDER_BOUNDS_T(kPF) __launch_bounds__(kRB, (kPF) ? RTX_WAVES_PER_SIMD_PF : RTX_WAVES_PER_SIMD)
 
 // Candidate list: per lane kCand slots in LDS, slot-major
 // (slot j of lane t at [j * kRB + t]: conflict-free), plus one dump slot
@@ -447,16 +494,11 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             }
             const uint32_t e = min(tb + kT, end);
             for (; b < e; ++b) {
-                const float4 *q = tl + 8u * (b - tb);
-                float4 v[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = q[t];
-                auto blk = [&](int i) {
-                    const float4 w = v[i >> 2];
-                    const int c = i & 3;
-                    return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
-                };
-                if (step(blk, b)) return b + 1;
+                // the block's floats straight from the tile where the step
+                // uses them (the compiler merges them into wide reads): a
+                // block staged whole in 32 VGPRs first spilled the lane state
+                const float *q = reinterpret_cast<const float *>(tl + 8u * (b - tb));
+                if (step([q](int i) { return q[i]; }, b)) return b + 1;
             }
             if (!more) break;
             tb += kT;
@@ -1295,19 +1337,7 @@ __device__ __forceinline__ void count_segments(const KParams &P, uint32_t segs) 
     if ((threadIdx.x & 63u) == 0u && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
 }
 
-__device__ __forceinline__ Frame load_frame(const KParams &P) {
-    Frame F;
-    F.org = mk3(P.org[0], P.org[1], P.org[2]);
-    F.hor = mk3(P.hor[0], P.hor[1], P.hor[2]);
-    F.ver = mk3(P.ver[0], P.ver[1], P.ver[2]);
-    F.llc = mk3(P.llc[0], P.llc[1], P.llc[2]);
-    F.img_w = P.img_w;
-    F.img_h = P.img_h;
-    F.lu = mk3(P.lens_u[0], P.lens_u[1], P.lens_u[2]);
-    F.lv = mk3(P.lens_v[0], P.lens_v[1], P.lens_v[2]);
-    F.lens_r = P.lens_r;
-    return F;
-}
+__device__ __forceinline__ Frame load_frame(const KParams &) { return Frame{}; }  // (frame_vals)
 
 // Start pixel `gid` (local index of this launch's rows) on this lane.
 // Launches with spp == 0 or depth == 0 never get here (k_render_trivial).
@@ -1725,6 +1755,38 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
     }
 }
 
+// Persistent cost pre-pass (large scenes): its tail. Once the pixel queue is
+// exhausted the pass runs on only until its last pixels' first samples end,
+// and at 100k spheres a lane-mode segment of a nearly idle GPU takes
+// milliseconds: the last ~20 % of the pass's time had most of the chip idle.
+// So the pass counts the pixels it has finished (pre_done, one atomic per
+// wave-iteration in which some ended), and once no more than pre_stop pixels
+// are still in flight, every wave stops its pixels where they are: each takes
+// the saturated key (the top bucket, as a pixel past the cost cap does) and
+// the render traces it from sample 0. Those are the pixels whose first sample
+// ran longest — the expensive ones — so the queue order they get is the right
+// one, and no result changes (the render redoes them with the same ops).
+__device__ __forceinline__ void pre_count(const KParams &P, uint64_t before, const Lane &L) {
+    const uint32_t n = (uint32_t)__popcll(before & ~__ballot(L.active));
+    if (n != 0u && (threadIdx.x & 63u) == 0u)
+        __hip_atomic_fetch_add(P.pre_done, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Returns true when it stopped the wave's pixels (wave-uniform).
+__device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &L) {
+    const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(P.pre_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint64_t act = __ballot(L.active);
+    if (act == 0ull || npix - min(done, npix) > P.pre_stop) return false;
+    if (L.active) {  // the cost cap's record: saturated key, restart from sample 0 (seed NaN)
+        P.cost_out[L.gid] = P.cost_capped;
+        P.state[L.gid] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0x7fc00000u));
+        L.segs = L.seg0;
+        L.active = false;
+        diag_pixel_end(P, L.gid);
+    }
+    pre_count(P, act, L);
+    return true;
+}
 // Render kernel (chain RNG), per-wave independent; sphere blocks are read
 // with scalar loads (a block-wide LDS copy serves the coop and the resolve of
 // scenes up to kCoopLds spheres). kPersist: the grid holds as many waves as the GPU keeps resident and
@@ -1732,7 +1794,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
 template <bool kPersist, bool kCost = false, bool kPF = false>
-__global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
+__global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][coop LDS copy of the spheres]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -1793,6 +1855,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         if (H.tier != 0u && __ballot(L.active) == 0ull) H.tier = 0;  // drained, no heavy slot left
         const bool heavy = H.tier != 0u;
         if (!heavy && !exhausted) exhausted = refill(P, F, kh, npix, L);
+        if (kPersist && kCost && P.pre_done && exhausted && pre_stop(P, npix, L)) continue;
         const uint64_t act = __ballot(L.active);
         D.section(0);
         if (act == 0ull) {  // spp, depth > 0: idle after both queues => drained
@@ -1845,6 +1908,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
             }
             if (prom_on)
                 written += (uint32_t)__popcll(act & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
+            if (kPersist && kCost && P.pre_done) pre_count(P, act, L);
             D.coop_end(cp, H.tier);
             if (H.tier == 0u) __builtin_amdgcn_s_setprio(0);  // a heavy wave keeps its priority
             D.section(3);
@@ -1880,6 +1944,7 @@ __global__ void RTX_RENDER_BOUNDS k_render(const KParams P) {
         D.section(2);
         if (prom_on)  // pixels written this iteration (promoted ones are counted by whoever finishes them)
             written += (uint32_t)__popcll(was_active & ~__ballot(L.active)) - (uint32_t)__popcll(__ballot(promoted));
+        if (kPersist && kCost && P.pre_done) pre_count(P, was_active, L);
     }
     D.finish(P);
     count_segments(P, L.segs);
@@ -2530,6 +2595,42 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     r[9] = (float)idx;
 }
 
+// Issue-rate probe of hit_world's own instruction mix (rtx_debug_scan_rate,
+// VERDICT r4 item 3): a full-occupancy grid of the render's shape (same
+// workgroup size, register budget and LDS: list, coop slots, the scene's LDS
+// copy) in which every lane takes one primary ray of the frame (pixel
+// gid * 7919 mod npix: a spread over the image) and runs k_render's lane-mode
+// hit_world on it `reps` times — the prefiltered scan and the resolve, nothing
+// else. Its VALU issue rate over the launch (SQ_INSTS_VALU / SIMD-cycles) is
+// what that mix sustains at the render's occupancy: the ceiling the render's
+// scan section can reach. Scenes up to kCoopLds spheres (the headline's).
+__global__ void RTX_RENDER_BOUNDS k_debug_scan_rate(const KParams P, uint32_t reps, unsigned long long *sink) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
+    uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kListBytes + kCoopBytes), true);
+    __syncthreads();
+    const uint32_t npix = P.rows_local * P.width;
+    const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
+    const uint32_t px = (uint32_t)(((uint64_t)gid * 7919u) % npix);
+    uint32_t x, y;
+    lane_pixel(P, px, x, y);
+    float seed = pixel_seed(P, x, y, 0);
+    f3 o, d;
+    start_sample(Frame{}, x, y, seed, o, d);
+    const float a = dir_len2(d);
+    const float inv_a = 1.0f / a;
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < reps; ++r) {
+        float best = __uint_as_float(0x7f800000u);
+        const int hit = hit_world_pre_ld<false>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, o, d, a, inv_a,
+                                                kTMin, best, list, nullptr, 0, RTX_SCAN_LDS ? sl.pr : nullptr);
+        acc += (uint32_t)hit ^ __float_as_uint(best);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += (uint32_t)__shfl_xor((int)acc, off, 64);
+    if ((threadIdx.x & 63u) == 0u) atomicAdd(sink, (unsigned long long)acc);
+}
+
 __global__ void __launch_bounds__(kBlock) k_debug_math(int fn, const float *in0, const float *in1,
                                                        uint32_t n, float *out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -2751,7 +2852,13 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         // ends takes the next one), so the pass does not wait on each wave's
         // slowest pixel — at 100k spheres an exact grid spent 27 % of the
         // C5 frame here; for small scenes the exact grid measured ~1 % faster
-        launch_k<true, true>(pf, min(need, resident_blocks(render_fn<true, true>(pf), lds)), lds, stream, c);
+        const uint32_t pblocks = min(need, resident_blocks(render_fn<true, true>(pf), lds));
+        // its tail: once at most pre_stop pixels are in flight they stop (pre_stop)
+        if (kPreStopFrac > 0.0) {
+            c.pre_done = sched.buckets + 2 * kCostBuckets + 6;  // heavy[6], zeroed above
+            c.pre_stop = (uint32_t)(kPreStopFrac * (double)pblocks * kRB);
+        }
+        launch_k<true, true>(pf, pblocks, lds, stream, c);
     } else {
         launch_k<false, true>(pf, need, lds, stream, c);
     }
@@ -2854,6 +2961,16 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
     if (nrays == 0) return hipSuccess;
     hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
                        rays, nrays, t_min, t_max, start_block, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
+                                  hipStream_t stream) {
+    if (p.scene.n > kCoopLds || use_pf(p.scene) || (uint64_t)p.rows_local * p.width == 0) return hipErrorInvalidValue;
+    const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n);
+    const uint32_t blocks = resident_blocks((const void *)k_debug_scan_rate, lds);
+    *waves = blocks * (kRB / 64);
+    hipLaunchKernelGGL(k_debug_scan_rate, dim3(blocks), dim3(kRB), lds, stream, p, reps, sink);
     return hipGetLastError();
 }
 

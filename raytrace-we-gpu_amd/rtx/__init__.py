@@ -137,11 +137,12 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_debug_math": (C.c_int, [ctx, C.c_int, f, f, u32, f]),
         "rtx_debug_wave_times": (C.c_int, [ctx, C.c_size_t, C.POINTER(C.c_uint64)]),
         "rtx_debug_pixel_cost": (C.c_int, [ctx, u32, C.POINTER(C.c_uint32)]),
+        "rtx_debug_scan_rate": (C.c_int, [ctx, u32, C.POINTER(C.c_float), C.POINTER(C.c_uint64)]),
     }
     # entry points added after 1.0 may be absent from older builds (A/B runs
     # of earlier libraries); calling one then fails with AttributeError
     optional = {"rtx_schedule_defaults", "rtx_set_schedule", "rtx_get_schedule", "rtx_debug_hit_world_from",
-                "rtx_build_info"}
+                "rtx_build_info", "rtx_debug_scan_rate"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(lib, name):
             continue
@@ -439,6 +440,13 @@ class Context:
         _check(self._lib.rtx_debug_wave_times(self._h, max_waves, out.ctypes.data_as(C.POINTER(C.c_uint64))),
                "rtx_debug_wave_times", self._lib)
         return out
+
+    def debug_scan_rate(self, reps: int) -> tuple:
+        """hit_world alone at the render's occupancy (rtx_debug_scan_rate):
+        (launch ms, wave-segments)."""
+        ms, ws = C.c_float(0.0), C.c_uint64(0)
+        _check(self._lib.rtx_debug_scan_rate(self._h, reps, C.byref(ms), C.byref(ws)), "rtx_debug_scan_rate")
+        return float(ms.value), int(ws.value)
 
     def debug_pixel_cost(self, spp: int = 0) -> np.ndarray:
         """Per-pixel ray-segment counts of the current frame, (H, W) uint32."""

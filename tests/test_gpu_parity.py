@@ -1126,3 +1126,22 @@ def test_upload_rejects_out_of_range_scene(gpu_ctx, rtx):
     with pytest.raises(rtx.RtxError):
         gpu_ctx.upload_world(bad)
     gpu_ctx.upload_world(w)
+
+
+def test_debug_scan_rate_probe(gpu_ctx, rtx):
+    """rtx_debug_scan_rate (the bench's issue-ceiling probe) runs the render's
+    hit_world at full occupancy and reports waves x reps; scenes beyond the
+    render's LDS copy (> 640 spheres) are refused, not run."""
+    W, H = 320, 180
+    world = rtx.random_world(11, depth=50, spp=16)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    gpu_ctx.upload_world(world)
+    gpu_ctx.set_frame(frame)
+    ms1, ws1 = gpu_ctx.debug_scan_rate(4)
+    ms2, ws2 = gpu_ctx.debug_scan_rate(8)
+    assert ms1 > 0.0 and ms2 > 0.0
+    assert ws1 > 0 and ws2 == 2 * ws1 and ws1 % 4 == 0
+    big = rtx.random_world(20, depth=50, spp=16)  # 1,600 spheres
+    gpu_ctx.upload_world(big)
+    with pytest.raises(rtx.RtxError):
+        gpu_ctx.debug_scan_rate(1)
