@@ -705,7 +705,9 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
         c->d_sched = nullptr;
         c->sched_pixels = 0;
         // cost, perm, buckets; then 16-byte aligned per-pixel state
-        RTX_HIP(hipMalloc(&c->d_sched, (sched_state_off(npix) + 4 * npix + 8 * (size_t)kPromCap) * sizeof(uint32_t)));
+        // ... the promotion queue, then the slot-ordered image staging (float4) and the inverse permutation
+        RTX_HIP(hipMalloc(&c->d_sched,
+                          (sched_state_off(npix) + 4 * npix + 8 * (size_t)kPromCap + 5 * npix) * sizeof(uint32_t)));
         // the promotion queue's epoch words start below every launch's epoch
         RTX_HIP(hipMemsetAsync(c->d_sched + sched_state_off(npix) + 4 * npix, 0,
                                8 * (size_t)kPromCap * sizeof(uint32_t), c->stream));
@@ -738,6 +740,8 @@ static int render_impl(rtx_ctx *c, uint32_t tile_rows, uint32_t part, uint32_t n
     sched.aux = c->aux_stream;
     sched.prom_q = c->d_sched + sched_state_off(c->sched_pixels) + 4 * c->sched_pixels;
     sched.prom_cap = kPromCap;
+    sched.stage = reinterpret_cast<float4 *>(sched.prom_q + 8 * (size_t)kPromCap);  // 16-byte aligned
+    sched.inv = sched.prom_q + 8 * (size_t)kPromCap + 4 * c->sched_pixels;
     sched.epoch = (uint32_t)++c->epoch;
     sched.ev_fork = c->ev_fork;
     sched.ev_join = c->ev_join;

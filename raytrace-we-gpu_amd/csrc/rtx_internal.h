@@ -49,6 +49,7 @@ constexpr uint32_t kErrPromTorn = 2u;     // a promotion entry held an out-of-ra
 struct KParams {
     KScene scene;
     float4 *out;                   // part's rows, contiguous, row-major
+    float4 *out_slot;              // cost-ordered render: the image by queue slot (k_unpermute), or NULL
     unsigned long long *counters;  // [0] += ray segments (hit_world calls)
     uint32_t *queue;               // pixel queue head (zeroed before each launch)
     uint32_t depth, spp;
@@ -127,6 +128,8 @@ struct KSchedule {
     uint32_t *cost;     // [npix]
     uint32_t *perm;     // [npix]
     float4 *state;      // [npix] (acc.xyz, seed) after the pre-pass's samples
+    float4 *stage;      // [npix] the render's image by queue slot (NULL: written in place)
+    uint32_t *inv;      // [npix] pixel -> queue slot (k_cost_scatter; k_unpermute)
     uint32_t *buckets;  // [2 * nbuckets + kSchedWords]: counts, cursors, heavy[8], prom[8] (zeroed per launch)
     uint32_t npix;      // capacity of cost / perm
     uint32_t nbuckets;  // must equal kCostBuckets of the kernel object

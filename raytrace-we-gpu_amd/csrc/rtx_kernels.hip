@@ -305,7 +305,10 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
 // loaded registers ("+s") so that nothing reads them before it. Every path
 // out of the loop body passes a wait, so no load is in flight at exit.
-constexpr uint32_t kScanPfMin = 1024;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
+#ifndef RTX_SCAN_PF_MIN  // (A/B builds: 0 sends every scene to the kPF kernels)
+#define RTX_SCAN_PF_MIN 1024
+#endif
+constexpr uint32_t kScanPfMin = RTX_SCAN_PF_MIN;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
 #ifndef RTX_PACK  // kPF scans start where the workgroup's other waves are (hit_world_pre_ld)
 #define RTX_PACK 1
 #endif
@@ -337,6 +340,9 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 #ifndef RTX_PF_LDS  // large scenes stream through a per-wave LDS tile of RTX_PF_LDS KiB (below; 0: SGPR double buffer)
 #define RTX_PF_LDS 1  // C5 1,880-1,907 -> 1,811-1,847 ms (profiles/R3w_*, R3x_*)
 #endif
+#ifndef RTX_PF_HALVES  // A/B: the tile scan stages a block in two halves (16 VGPRs) instead of whole (32)
+#define RTX_PF_HALVES 0
+#endif
 #ifndef RTX_PF_RING  // A/B: the tile stream as a ring of RTX_PF_RING 1-KiB slots filled by LDS-DMA (0: VGPR staging)
 #define RTX_PF_RING 0
 #endif
@@ -358,10 +364,13 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base) {
                  : "v"(gsrc), "s"(lds_base)
                  : "memory");
 }
+#ifndef RTX_SCAN_PREFETCH  // A/B build: the small-scene scan double-buffers its blocks in SGPRs like kPF's
+#define RTX_SCAN_PREFETCH 0
+#endif
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
 #define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
 #endif
-template <bool kPF, bool kFlat>
+template <bool kPF, bool kFlat, bool kTile = false>
 __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_t end, const LineTest &T,
                                                float k0, float k1, uint32_t *my, uint32_t &cnt, bool &full,
                                                uint32_t *pack, const float *lds_pr) {
@@ -417,7 +426,10 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
         return finish(q, bb);
     };
     full = true;
-    if (kPF && RTX_PF_RING && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
+    // kTile (k_render's large-scene lane mode, which passes its tile): the
+    // tile stream is the only scan instantiated there, so the SGPR ping-pong
+    // below (64 SGPRs) does not crowd that kernel's registers
+    if (kTile && kPF && RTX_PF_RING && lds_pr != nullptr) {
         // A/B build: the scene streams through a ring of
         // kNR 1-KiB slots (8 blocks each) per wave, filled by LDS-DMA with no
         // VGPR staging: kNR - 1 tiles in flight while one is scanned. Before
@@ -463,7 +475,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             tb += 8u;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (kPF && RTX_PF_LDS && lds_pr != nullptr) {  // (wave-uniform: k_render's lane mode passes its tile)
+    } else if (kTile && kPF && RTX_PF_LDS && lds_pr != nullptr) {
         // A/B build: the scene streams through a per-wave
         // LDS tile of 8 * RTX_PF_LDS blocks (RTX_PF_LDS KiB: coalesced 16-byte
         // loads, one per lane per KiB, the next tile's loads in flight while
@@ -494,16 +506,34 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             }
             const uint32_t e = min(tb + kT, end);
             for (; b < e; ++b) {
-                // the block's floats straight from the tile where the step
-                // uses them (the compiler merges them into wide reads): a
-                // block staged whole in 32 VGPRs first spilled the lane state
-                const float *q = reinterpret_cast<const float *>(tl + 8u * (b - tb));
-                if (step([q](int i) { return q[i]; }, b)) return b + 1;
+                // (reading the floats at their use instead of staging the
+                // block in 8 VGPR quads measured 7 % slower at C5: R7b)
+                const float4 *q = tl + 8u * (b - tb);
+                if (RTX_PF_HALVES) {  // A/B: the block in two halves of 4 quads (spheres 0-3, then 4-7)
+                    f2v qq[4];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float4 cx = q[h], cy = q[2 + h], cz = q[4 + h], rr = q[6 + h];
+                        qq[2 * h] = qpair(f2v{cx.x, cx.y}, f2v{cy.x, cy.y}, f2v{cz.x, cz.y}, f2v{rr.x, rr.y});
+                        qq[2 * h + 1] = qpair(f2v{cx.z, cx.w}, f2v{cy.z, cy.w}, f2v{cz.z, cz.w}, f2v{rr.z, rr.w});
+                    }
+                    if (finish(qq, b)) return b + 1;
+                    continue;
+                }
+                float4 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = q[t];
+                auto blk = [&](int i) {
+                    const float4 w = v[i >> 2];
+                    const int c = i & 3;
+                    return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
+                };
+                if (step(blk, b)) return b + 1;
             }
             if (!more) break;
             tb += kT;
         }
-    } else if (kPF) {
+    } else if (!kTile && (kPF || RTX_SCAN_PREFETCH)) {
         // ping-pong between two SGPR buffers (no copies): A holds block b
         f16v a_lo, a_hi, b_lo, b_hi;
         sload_blk(pre + 32 * b, a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
@@ -521,7 +551,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             // the wrapped leg of a segment. Publishing from both halves (every
             // scan) measured no faster than no pack at all, this 4-7 % faster
             // (DESIGN.md §7 R4k-q).
-            if (RTX_PACK && (b & (kPackEvery - 1u)) == 0u && (threadIdx.x & 63u) == 0u) *pack = b;
+            if (kPF && RTX_PACK && pack && (b & (kPackEvery - 1u)) == 0u && (threadIdx.x & 63u) == 0u) *pack = b;
             sload_blk(pre + 32 * min(b + 1, end - 1), a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
             f = step([&](int i) { return i < 16 ? b_lo[i] : b_hi[i - 16]; }, b);
             sload_wait(a_lo, a_hi);
@@ -558,7 +588,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
 // (rtx_internal.h KScene) with the 5-op test, the rest with the 7-op one.
 // Returns the block to resume at: nblk, or earlier once some lane's list is
 // full (wave-uniform). kPF scans publish their position to `pack` (below).
-template <bool kPF>
+template <bool kPF, bool kTile = false>
 __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk, const LineTest &T,
                                                    const KScene &S, uint32_t *list, uint32_t &cnt,
                                                    uint32_t *pack = nullptr, const float *lds_pr = nullptr) {
@@ -568,11 +598,11 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
     while (b < nblk) {
         bool full;
         if (b < S.flat_lo) {
-            b = scan_range<kPF, false>(pre, b, min(S.flat_lo, nblk), T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
+            b = scan_range<kPF, false, kTile>(pre, b, min(S.flat_lo, nblk), T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         } else if (b < S.flat_hi) {
-            b = scan_range<kPF, true>(pre, b, min(S.flat_hi, nblk), T, K.ku, K.kv, my, cnt, full, pack, lds_pr);
+            b = scan_range<kPF, true, kTile>(pre, b, min(S.flat_hi, nblk), T, K.ku, K.kv, my, cnt, full, pack, lds_pr);
         } else {
-            b = scan_range<kPF, false>(pre, b, nblk, T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
+            b = scan_range<kPF, false, kTile>(pre, b, nblk, T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         }
         if (full) break;
     }
@@ -691,7 +721,7 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // waves that trail it, instead of every wave missing on every block.
 // start (no pack word): the block to start at (rtx_debug_hit_world_from),
 // wave-uniform.
-template <bool kPF, typename Ld>
+template <bool kPF, typename Ld, bool kTile = false>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
                                                 float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
                                                 uint32_t start = 0, const float *lds_pr = nullptr,
@@ -714,7 +744,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     uint32_t b = b0, end = nblk;
     for (;;) {
         uint32_t cnt;
-        b = scan_prefilter<kPF>(pre, b, end, T, S, list, cnt, pack, lds_pr);
+        b = scan_prefilter<kPF, kTile>(pre, b, end, T, S, list, cnt, pack, lds_pr);
         ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
         if (b < end) continue;
         if (end == nblk && b0 != 0u) {  // wrap round to the start
@@ -1040,8 +1070,11 @@ __device__ __forceinline__ void begin_sample(const KParams &P, const Frame &F, u
 }
 
 // accColor /= spp; toGamma; float4(c, 1) (:312-314) for local pixel gid,
-// whose linear sample sum is `sum`.
-__device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 sum) {
+// whose linear sample sum is `sum`. `slot`: the pixel's queue slot in a
+// cost-ordered render with a slot-ordered staging image (KParams::out_slot):
+// the pixel goes to out_slot[slot] and k_unpermute moves it to out[gid] with
+// coalesced stores; ~0u (or no staging): straight to out[gid].
+__device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 sum, uint32_t slot = ~0u) {
     float n = (float)P.spp;
     if (P.accum) {  // progressive: running linear sum over frames
         float4 a = P.accum[gid];
@@ -1057,7 +1090,10 @@ __device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 
     o.y = to_gamma(sum.y / n);
     o.z = to_gamma(sum.z / n);
     o.w = 1.0f;
-    P.out[gid] = o;
+    if (P.out_slot && slot != ~0u)
+        P.out_slot[slot] = o;
+    else
+        P.out[gid] = o;
 }
 
 #ifndef RTX_EXTRA_BYTES
@@ -1072,7 +1108,7 @@ __device__ __forceinline__ void write_pixel(const KParams &P, const Lane &L) {
         if (P.state) P.state[L.gid] = make_float4(L.acc.x, L.acc.y, L.acc.z, L.seed);
         return;
     }
-    output_pixel(P, L.gid, L.acc);
+    output_pixel(P, L.gid, L.acc, L.slot);
     // A/B build (HBM traffic): the pixel's final state also
     // goes back to its (dead) resume slot: +16 B per pixel of the same
     // scattered cost-order stores as the image
@@ -1270,6 +1306,9 @@ __device__ __forceinline__ bool promote(const KParams &P, const Lane &L, uint32_
     if ((uint64_t)segs * (P.spp - L.sample) <= (uint64_t)min_segs * done) return false;
     const uint32_t slot = atomicAdd(&P.prom[0], 1u);
     if (slot >= P.prom_cap) return false;  // queue full: the lane keeps its pixel
+    // whoever finishes a promoted pixel writes it to out[gid] directly: its
+    // staging slot says so (w = 0; an output pixel's w is 1), k_unpermute skips it
+    if (P.out_slot && L.slot != ~0u) P.out_slot[L.slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint32_t *e = P.prom_q + 8u * slot;
     __hip_atomic_store(e + 0, L.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(e + 1, L.sample, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1476,6 +1515,7 @@ __device__ __forceinline__ bool take_from(const KParams &P, const Frame &F, uint
     const uint32_t rk = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
     if (!L.active && rk < take) {
         start_pixel(P, F, P.perm[h + rk], L);
+        L.slot = h + rk;
         diag_pixel_start(P, L.gid, ctr == P.heavy ? 1ull : 2ull);
     }
     if (h + room >= hi) done = true;
@@ -1896,9 +1936,9 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
                                   : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
                                                      coop_ws, my_best, my_seq, cp, ctqp);
             if (L.active) {
-                if (my_seq) {
+                if (my_seq) {  // (rare: the plain scan, so the kPF ping-pong's SGPRs stay out of this kernel)
                     my_best = __uint_as_float(0x7f800000u);
-                    my_hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
+                    my_hit = hit_world_pre<false>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
                 // the tail's pixels may be promoted (tier-1 waves already
                 // trace one ray with every lane; promoting tier-2 pixels
@@ -1925,8 +1965,9 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         bool promoted = false;
         if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
             float best = __uint_as_float(0x7f800000u);
-            const int hit = hit_world_pre_ld<kPF>(P.scene, [&P](uint32_t i) { return P.scene.cen[i]; }, L.o, L.d, L.a,
-                                                  L.inv_a, kTMin, best, list, nullptr, 0, pf_tile, L.active);
+            auto ldc = [&P](uint32_t i) { return P.scene.cen[i]; };
+            const int hit = hit_world_pre_ld<kPF, decltype(ldc), true>(P.scene, ldc, L.o, L.d, L.a, L.inv_a, kTMin,
+                                                                       best, list, nullptr, 0, pf_tile, L.active);
             D.section(1);
             if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
         } else if (L.active) {
@@ -2212,7 +2253,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          uint32_t cost_spp, uint32_t sat_cap,
                                                          const uint32_t *counts, uint32_t *cursors,
-                                                         uint32_t *perm) {
+                                                         uint32_t *perm, uint32_t *inv) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -2238,7 +2279,11 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     __syncthreads();
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
         const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) perm[start[key[k]] + rank[k]] = i;
+        if (i < n) {
+            const uint32_t g = start[key[k]] + rank[k];
+            perm[g] = i;
+            if (inv) inv[i] = g;  // coalesced: pixel i's queue slot (k_unpermute)
+        }
     }
 }
 
@@ -2555,6 +2600,18 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
     const uint32_t part = tile % nparts;
     const uint32_t lr = (tile / nparts) * tile_rows + (y - tile * tile_rows);
     img[i] = g[((uint64_t)part * max_rows + lr) * width + x];
+}
+
+// The cost-ordered render's image, from its slot-ordered staging buffer to
+// the linear framebuffer (ShaderCompute.hlsl:314's one texel per pixel, in
+// pixel order): pixel i is stage[inv[i]], read gathered, stored coalesced; a
+// promoted pixel (stage w = 0) was written to out[i] by whoever finished it.
+__global__ void __launch_bounds__(kBlock) k_unpermute(const float4 *__restrict__ stage, const uint32_t *__restrict__ inv,
+                                                      uint32_t npix, float4 *__restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= npix) return;
+    const float4 v = stage[inv[i]];
+    if (v.w != 0.0f) out[i] = v;
 }
 
 // t_min > 0 and t_max >= t_min (rtx_debug_hit_world checks): the resolve
@@ -2878,10 +2935,12 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, p.spp,
                        heavy, tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, split_cap, sched.buckets, sched.buckets + kCostBuckets, sched.perm);
+                       p.rows_local, c.spp, split_cap, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
+                       sched.stage ? sched.inv : nullptr);
     KParams q = p;
     q.cost_spp = c.spp;
     q.perm = sched.perm;
+    q.out_slot = sched.stage;  // the image in queue-slot order, k_unpermute after the render
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
@@ -2943,6 +3002,11 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     launch_k<true, false>(pf, blocks, lds, stream, q);
     e = hipGetLastError();
     if (e == hipSuccess && trace_waves > 0) e = hipStreamWaitEvent(stream, sched.ev_join, 0);
+    if (e == hipSuccess && sched.stage) {
+        hipLaunchKernelGGL(k_unpermute, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, sched.stage, sched.inv,
+                           (uint32_t)lanes, p.out);
+        e = hipGetLastError();
+    }
     return e;
 }
 
