@@ -37,6 +37,8 @@ for s in $STEPS; do
                 python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pmc off --parts '' --per-sample 0 ;;
     prof8)  run prof8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof8" -o run -- \
                 python3 bench.py --probe --probe-parts 8 ;;
+    c5prof) run c5prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5prof" -o run -- \
+                python3 bench.py --probe --spp 16 --grid 159 --max-spheres 100000 --probe-frames 2 ;;
     psprof) run psprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/psprof" -o run -- \
                 python3 bench.py --probe --rng per-sample --probe-frames 3 ;;
     gtest)  run gtest 600 python -u -m pytest ${GTESTS:-tests/test_gpu_parity.py} -m gpu -x -q --timeout 120 \
