@@ -151,7 +151,7 @@ def _pmc_pass(args, counters, tag, rng=None, extra=()):
         shutil.rmtree(out, ignore_errors=True)
 
 
-def pmc_traffic(args):
+def pmc_traffic(args, rng=None):
     """HBM bytes per render launch from rocprofv3 PMC counters, per
     MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes
     (TCC slots), KB units, FETCH_SIZE x2 on gfx950 for wide coalesced reads.
@@ -159,8 +159,8 @@ def pmc_traffic(args):
     (pre-pass, sort, render, k_trace). Returns (bytes, details) or (None,
     reason)."""
     try:
-        f = _pmc_pass(args, ["FETCH_SIZE"], "fetch")
-        w = _pmc_pass(args, ["WRITE_SIZE"], "write")
+        f = _pmc_pass(args, ["FETCH_SIZE"], "fetch", rng)
+        w = _pmc_pass(args, ["WRITE_SIZE"], "write", rng)
     except RuntimeError as e:
         return None, str(e)
     fetch, write = f["FETCH_SIZE"], w["WRITE_SIZE"]
@@ -580,10 +580,13 @@ def main():
             st_ps = ctx.stats()
             ps_ms = st_ps.kernel_ms / max(1, st_ps.launches)
             ps_exec = pmc_valu(args, n_cu, ps_ms, rng="per-sample") if args.pmc == "auto" else None
+            ps_traffic, ps_pmc = pmc_traffic(args, rng="per-sample") if args.pmc == "auto" else (None, "skipped")
             per_sample = {"value": round(W * H * args.spp / t_ps / 1e6, 3), "unit": "Msamples/s",
                           "ms_per_step": round(t_ps * 1e3, 3), "steps": n_ps, "kernel_ms": round(ps_ms, 4),
                           "roofline": roofline_of(ps_exec, ps_ms, st_ps.sphere_tests / max(1, st_ps.launches)),
                           "executed": ps_exec,
+                          "traffic": None if ps_traffic is None else round(ps_traffic), "pmc": ps_pmc,
+                          "measured_hbm_GBs": None if ps_traffic is None else round(ps_traffic / (ps_ms * 1e-3) / 1e9, 3),
                           "kernel": launch_desc(world.count, args.spp, R, "per-sample")}
             if args.cpu_seconds > 0:
                 rows_ps = [int(r) for r in np.linspace(5, H - 6, 16)]  # 16 rows spread over the image

@@ -1715,7 +1715,8 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
 // but live chain — a big scene, a high spp — never trips the valve however
 // long it runs without another pixel finishing; only a launch in
 // which nothing traces any more does. The stress build (make all) runs with
-// a 2 ms valve, so its GPU tests exercise exactly that.
+// a 20 ms valve (a beat every 1.25 ms), so its GPU tests exercise exactly
+// that.
 #ifndef RTX_PROM_VALVE_TICKS
 #define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s of s_memrealtime (100 MHz)
 #endif
@@ -1918,7 +1919,11 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
             continue;
         }
         const uint64_t was_active = act;
-        if (prom_on && (exhausted || H.tier != 0u)) beat(P, last_beat);  // still tracing: the valve sees progress
+        // still tracing: the servers' valve sees progress. Every tracing wave
+        // beats, not only those that have seen the queue exhausted: a wave
+        // whose lanes are all busy never refills and never learns it (R7e: a
+        // 2 ms stress valve fired while only such waves were tracing)
+        if (prom_on) beat(P, last_beat);
         D.iteration(act);
         if (heavy || (exhausted && (uint32_t)__popcll(act) <= P.coop_max)) {
             D.tail_iteration();
