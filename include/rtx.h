@@ -256,7 +256,7 @@ typedef struct rtx_schedule {
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
     uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
-    uint32_t trace_group;     /* default 4: tier-1 pixels per wave of the tier-1 kernel (1, 2 or 4) */
+    uint32_t trace_group;     /* default 4: tier-1 pixels per wave of the tier-1 kernel (1, 2, 4 or 8; 8 since 1.4.1) */
     uint32_t prepass_cap_split; /* default 0 (none): a row-split part's cost pre-pass stops a pixel past this
                                    many segments (0..4096); it goes to the top of the queue (tier 1) and the
                                    render traces it from sample 0 */
@@ -271,7 +271,7 @@ RTX_API int rtx_schedule_defaults(rtx_schedule *out);
  * the defaults): bars and shares finite and > 0, hot_fraction in [0, 1],
  * occupancies in (0, 1], trace_* in [0, 0.5], promote_* in [0, 1e9],
  * tail_coop_max and tail_coop_max_large in 1..64,
- * priorities in 0..3, refill_chunk in 0..4096, trace_group 1, 2 or 4,
+ * priorities in 0..3, refill_chunk in 0..4096, trace_group 1, 2, 4 or 8,
  * trace_solo_bar > 0, prepass_cap_split in 0..4096, prio_bar1 = 0 or
  * 0 < prio_bar1 <= prio_bar2 <= prio_bar3 <= 1e30, reserved 0. */
 RTX_API int rtx_set_schedule(rtx_ctx *ctx, const rtx_schedule *schedule);

@@ -343,8 +343,8 @@ int rtx_set_schedule(rtx_ctx *c, const rtx_schedule *s) {
     if (s->tier1_priority > 3 || s->tier2_priority > 3 || s->hot_priority > 3)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: priorities must be in 0..3");
     if (s->refill_chunk > 4096) return fail(RTX_ERR_INVALID, "rtx_set_schedule: refill_chunk must be in 0..4096");
-    if (s->trace_group != 1 && s->trace_group != 2 && s->trace_group != 4)
-        return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_group must be 1, 2 or 4");
+    if (s->trace_group != 1 && s->trace_group != 2 && s->trace_group != 4 && s->trace_group != 8)
+        return fail(RTX_ERR_INVALID, "rtx_set_schedule: trace_group must be 1, 2, 4 or 8");
     if (s->prepass_cap_split > 4096)
         return fail(RTX_ERR_INVALID, "rtx_set_schedule: prepass_cap_split must be in 0..4096");
     if (!(s->prio_bar1 == 0.0f || (s->prio_bar1 > 0.0f && s->prio_bar1 <= s->prio_bar2 &&

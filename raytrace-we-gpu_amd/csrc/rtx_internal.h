@@ -117,7 +117,7 @@ struct KTune {
     double trace_small, trace_low, trace_medium, trace_large;  // k_trace waves / resident waves, by share class
     double prom_small, prom_low, prom_medium, prom_large;      // promotion threshold (projected segments; 0: off)
     double prom_big;                                           // ... for scenes without the coop's LDS copy
-    uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2 or 4)
+    uint32_t trace_group;                                      // k_trace: pixels per wave (1, 2, 4 or 8)
     double trace_solo;                                         // ... one per wave above this x share (k0)
     uint32_t cap_split;                                        // pre-pass cap of a row-split part (0: none)
     double dyn1, dyn2, dyn3;  // lane-mode wave priority 1/2/3 above these x the mean pixel (dyn1 0: static hot slots)

@@ -149,7 +149,7 @@ constexpr double kPromSmall = 400.0, kPromLow = 300.0, kPromMedium = 400.0, kPro
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;
-// k_trace: tier-1 pixels per wave (1, 2 or 4: rtx_set_schedule), and the key bar (x share)
+// k_trace: tier-1 pixels per wave (1, 2, 4 or 8: rtx_set_schedule), and the key bar (x share)
 // above which a pixel is traced alone in its wave nonetheless
 constexpr uint32_t kTraceGroup = 4;
 constexpr double kTraceSolo = 6.0;
@@ -2109,7 +2109,7 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     const uint32_t k1 = min(P.heavy[3], min(P.heavy[1], npix));
     const uint32_t k0 = min(P.heavy[4], k1);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lg_many = min(max(P.trace_lg, 4u), 6u);
+    const uint32_t lg_many = min(max(P.trace_lg, 3u), 6u);
     set_prio(P.prio_t1);
     uint32_t lg = 6u;
     Lane W;
@@ -2185,10 +2185,12 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             if (first) segs += n;
         } else {
             if (P.prom) beat(P, last_beat);
-            if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 (rtx_set_schedule)
+            if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 or 8 (rtx_set_schedule)
                 trace_group_segment<5>(P, F, sl, W, ended);
-            else
+            else if (lg == 4u)
                 trace_group_segment<4>(P, F, sl, W, ended);
+            else  // 8 pixels per wave, 8 lanes each: a third of the issue per pixel-segment of 16-lane groups
+                trace_group_segment<3>(P, F, sl, W, ended);
             if (W.active && first) segs++;
         }
         if (ended) {

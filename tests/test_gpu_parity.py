@@ -796,7 +796,7 @@ def test_schedule_validation_and_extremes(gpu_ctx, oracle, rtx):
     d = rtx.schedule_defaults()
     for field, bad in (("tier1_bar", 0.0), ("tier2_bar_small", float("nan")), ("small_share", -1.0),
                        ("hot_fraction", 1.5), ("occupancy_low", 0.0), ("occupancy_normal", 1.01),
-                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_group", 0), ("trace_group", 3), ("trace_group", 8), ("trace_solo_bar", 0.0), ("prepass_cap_split", 5000), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
+                       ("tail_coop_max", 0), ("tail_coop_max", 65), ("tail_coop_max_large", 0), ("tail_coop_max_large", 65), ("tier1_priority", 4), ("trace_group", 0), ("trace_group", 3), ("trace_group", 16), ("trace_solo_bar", 0.0), ("prepass_cap_split", 5000), ("trace_low", 0.6), ("trace_small", -0.1), ("promote_low", -1.0), ("promote_big_scene", -1.0), ("refill_chunk", 5000),
                        ("prio_bar1", -1.0), ("prio_bar1", 2.0), ("prio_bar2", 0.2), ("prio_bar3", float("nan")),
                        ("reserved", 1)):
         with pytest.raises(rtx.RtxError):
@@ -842,7 +842,7 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
     empty a lane hands its pixel to k_trace at a sample boundary (threshold 1
     projected segment: nearly every pixel still in flight is handed over,
     the 65,536-entry queue overflows on the whole frame and lanes keep the
-    rest). k_trace with 1, 2 and 4 pixels per wave (trace_group), the
+    rest). k_trace with 1, 2, 4 and 8 pixels per wave (trace_group), the
     heaviest alone (trace_solo_bar). Whole frames and row-tile shares of
     every size class, against the oracle bit for bit, and the frame's
     segment count."""
@@ -869,6 +869,10 @@ def test_trace_kernel_and_promotion_bit_exact(request, oracle, rtx, ctx_name):
                   dict(trace_small=0.05, trace_low=0.05, trace_medium=0.05, trace_large=0.05, tier1_bar=1.0,
                        tier1_bar_small=1.0, tier1_bar_low=1.0, trace_group=4, trace_solo_bar=2.5,
                        promote_small=1, promote_low=1, promote_medium=1, promote_large=1),
+                  # groups of 8 lanes (8 pixels per wave), promotion served by them
+                  dict(trace_small=0.2, trace_low=0.2, trace_medium=0.2, trace_large=0.2, tier1_bar=1.0,
+                       tier1_bar_small=1.0, tier1_bar_low=1.0, trace_group=8, trace_solo_bar=3.0,
+                       promote_small=30, promote_low=30, promote_medium=30, promote_large=30),
                   # a row-split share's pre-pass stops pixels past 6 segments: they restart from
                   # sample 0 in tier 1 (k_trace), their neighbours' keys count the cap
                   dict(trace_small=0.25, trace_low=0.2, trace_group=2, prepass_cap_split=6, promote_small=100,
