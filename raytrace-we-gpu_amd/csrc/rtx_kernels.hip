@@ -340,9 +340,6 @@ __device__ __forceinline__ void sload_wait(f16v &lo, f16v &hi) {
 #ifndef RTX_PF_LDS  // large scenes stream through a per-wave LDS tile of RTX_PF_LDS KiB (below; 0: SGPR double buffer)
 #define RTX_PF_LDS 1  // C5 1,880-1,907 -> 1,811-1,847 ms (profiles/R3w_*, R3x_*)
 #endif
-#ifndef RTX_PF_HALVES  // A/B: the tile scan stages a block in two halves (16 VGPRs) instead of whole (32)
-#define RTX_PF_HALVES 0
-#endif
 #ifndef RTX_PF_RING  // A/B: the tile stream as a ring of RTX_PF_RING 1-KiB slots filled by LDS-DMA (0: VGPR staging)
 #define RTX_PF_RING 0
 #endif
@@ -364,9 +361,6 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base) {
                  : "v"(gsrc), "s"(lds_base)
                  : "memory");
 }
-#ifndef RTX_SCAN_PREFETCH  // A/B build: the small-scene scan double-buffers its blocks in SGPRs like kPF's
-#define RTX_SCAN_PREFETCH 0
-#endif
 #ifndef RTX_SCAN_LDS  // A/B build: the small-scene scan reads its blocks from the block's LDS copy
 #define RTX_SCAN_LDS 0  // (broadcast ds_read_b128, 8 per block) instead of scalar loads
 #endif
@@ -506,20 +500,9 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             }
             const uint32_t e = min(tb + kT, end);
             for (; b < e; ++b) {
-                // (reading the floats at their use instead of staging the
-                // block in 8 VGPR quads measured 7 % slower at C5: R7b)
+                // (reading the floats at their use, or staging the block in
+                // two halves, measured 7 % slower at C5: R7b, R7d)
                 const float4 *q = tl + 8u * (b - tb);
-                if (RTX_PF_HALVES) {  // A/B: the block in two halves of 4 quads (spheres 0-3, then 4-7)
-                    f2v qq[4];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const float4 cx = q[h], cy = q[2 + h], cz = q[4 + h], rr = q[6 + h];
-                        qq[2 * h] = qpair(f2v{cx.x, cx.y}, f2v{cy.x, cy.y}, f2v{cz.x, cz.y}, f2v{rr.x, rr.y});
-                        qq[2 * h + 1] = qpair(f2v{cx.z, cx.w}, f2v{cy.z, cy.w}, f2v{cz.z, cz.w}, f2v{rr.z, rr.w});
-                    }
-                    if (finish(qq, b)) return b + 1;
-                    continue;
-                }
                 float4 v[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) v[t] = q[t];
@@ -533,7 +516,7 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
             if (!more) break;
             tb += kT;
         }
-    } else if (!kTile && (kPF || RTX_SCAN_PREFETCH)) {
+    } else if (!kTile && kPF) {  // (the same for small scenes measured 6 % slower: R7c)
         // ping-pong between two SGPR buffers (no copies): A holds block b
         f16v a_lo, a_hi, b_lo, b_hi;
         sload_blk(pre + 32 * b, a_lo, a_hi, ux, uy, uz, vy, vz, ku, kv);
