@@ -59,6 +59,10 @@ def parse():
                    help="also time the per-sample-RNG kernel on the same frame (N=1, chain runs only)")
     p.add_argument("--parts", default="2,4,8",
                    help="N=1: time every part of these R-way row-tile splits on this device ('' = skip)")
+    p.add_argument("--gather", action="store_true",
+                   help="N=1: run the N-rank path anyway (process group over RCCL, row tiles, one gather, "
+                        "de-interleave): a one-GPU rehearsal of it")
+    p.add_argument("--dump-image", default="", help=argparse.SUPPRESS)  # rank 0 saves the last frame (.npy)
     p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--probe-parts", type=int, default=0, help=argparse.SUPPRESS)  # --probe: an R-way split
     p.add_argument("--probe-frames", type=int, default=1, help=argparse.SUPPRESS)  # --probe: whole frames
@@ -484,7 +488,13 @@ def main():
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
         args.gpus = world_size
     torch.cuda.set_device(local_rank)
-    if world_size > 1:
+    collective = world_size > 1 or args.gather
+    if collective:
+        if world_size == 1:  # --gather outside torch.distributed.run: a one-rank group
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     world, frame = scene_and_frame(args)
@@ -498,14 +508,14 @@ def main():
     ctx.upload_world(world)
     ctx.set_frame(frame)
     dev = torch.device("cuda", local_rank)
-    if R == 1:
+    if not collective:
         image = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
 
         def step():
             ctx.render_rows(1, 0, 1, image.data_ptr())
     else:
         from rtx.dist import FrameGather
-        fg = FrameGather(W, H, T, rank, R, device=dev,
+        fg = FrameGather(W, H, T, rank, R, device=dev, collective=True,
                          render_part=lambda send, part, nparts: ctx.render_rows(T, part, nparts, send.data_ptr()),
                          deinterleave=lambda g, img: ctx.deinterleave(g.data_ptr(), W, H, T, R, img.data_ptr()))
         image = fg.image
@@ -514,7 +524,7 @@ def main():
             fg.step()
 
     def barrier():
-        if R > 1:
+        if collective:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -529,11 +539,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    if R > 1:
+    if collective:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = ctx.stats()
+    if args.dump_image and rank == 0:
+        np.save(args.dump_image, image.cpu().numpy())
 
     if rank == 0:
         samples = W * H * args.spp * args.steps
@@ -616,7 +628,7 @@ def main():
                                    f"{world.count} spheres, {args.rng} RNG",
                        "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                        "spheres": world.count, "rng": args.rng, "tile_rows": T,
-                       "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if R > 1 else "")},
+                       "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if collective else "")},
             "roofline": roof,
             "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -636,7 +648,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     ctx.close()
-    if R > 1:
+    if collective:
         dist.destroy_process_group()
 
 

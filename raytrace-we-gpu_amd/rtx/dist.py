@@ -47,7 +47,7 @@ class FrameGather:
 
     def __init__(self, width: int, height: int, tile_rows: int, rank: int, world_size: int,
                  render_part: Callable, deinterleave: Optional[Callable] = None,
-                 device=None, root: int = 0):
+                 device=None, root: int = 0, collective: bool = False):
         import torch
         self.W, self.H, self.T, self.rank, self.R, self.root = width, height, tile_rows, rank, world_size, root
         self.max_rows = part_rows(height, tile_rows, 0, world_size)  # part 0 is the largest
@@ -58,11 +58,15 @@ class FrameGather:
         self.image = torch.zeros((height, width, 4), **kw) if rank == root else None
         self.render_part = render_part
         self.deinterleave = deinterleave
+        # collective: gather through the process group even with one rank (a
+        # one-GPU rehearsal of the N-rank path: RCCL's gather on the render's
+        # buffers, the same stream order)
+        self.collective = collective or world_size > 1
 
     def step(self):
         import torch.distributed as dist
         self.render_part(self.send, self.rank, self.R)
-        if self.R > 1:
+        if self.collective:
             gl = list(self.gathered.unbind(0)) if self.rank == self.root else None
             dist.gather(self.send, gather_list=gl, dst=self.root)
         elif self.rank == self.root:

@@ -98,3 +98,30 @@ def test_multirank_gather_with_the_kernel(tmp_path, gpu_ctx, oracle, rtx, world_
     rows = np.linspace(1, H - 2, 8).astype(np.uint32)
     want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
     np.testing.assert_array_equal(got[rows].view(np.uint32), want.view(np.uint32))
+
+
+def test_bench_rccl_path_one_rank(tmp_path, oracle, rtx):
+    """bench.py's N-rank path (process group over RCCL — torch.distributed
+    "nccl" —, the render into the rank's row-tile send buffer, ONE RCCL gather,
+    rtx_deinterleave_rows, all ordered on one torch stream handed to librtx)
+    run with one rank on the box's GPU (`--gather`): the driver's 8-GPU run is
+    the only other place it executes. The line must carry the RCCL
+    parallelism and the gathered frame must equal the oracle's rows."""
+    import json
+    import subprocess
+    W, H, spp = 320, 180, 16
+    img_path = str(tmp_path / "img.npy")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--gather", "--width", str(W),
+           "--height", str(H), "--spp", str(spp), "--steps", "2", "--warmup", "1", "--pmc", "off",
+           "--cpu-seconds", "0", "--parts", "", "--per-sample", "0", "--dump-image", img_path]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["config"]["parallelism"] == "row-tiles x1 + RCCL gather"
+    got = np.load(img_path)
+    world = rtx.random_world(11, depth=50, spp=spp)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    rows = np.linspace(1, H - 2, 8).astype(np.uint32)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(got[rows].view(np.uint32), want.view(np.uint32))
