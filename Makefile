@@ -61,13 +61,15 @@ clean:
 #   prof   - per-section clock sums (tools/section_prof.py)
 #   ptime  - per-pixel start/end times (tools/pixel_timeline.py)
 #   cprof  - per-section clocks of tier-1 coop segments (tools/coop_prof.py)
+#   rays   - a sample of lane-mode wave iterations' rays (tools/ray_sample.py)
 # Ad-hoc A/B builds for tools/variant_bench.py:
 #   make adhoc V=name VFLAGS="-DRTX_...=..."   -> lib/variants/librtx_name.so
-VARIANTS := stress prof ptime cprof
+VARIANTS := stress prof ptime cprof rays
 VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=2000000ull
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
+VFLAGS_rays          := -DRTX_DIAG_RAYS=4099
 VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)

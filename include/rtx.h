@@ -38,8 +38,10 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 141 /* 1.4.1 */
+#define RTX_VERSION 142 /* 1.4.2 */
 /* ABI notes.
+ *  1.4.2: rtx_debug_hit_world_from's start_block RTX_DEBUG_CULLED (the
+ *         culled scan; no layout change).
  *  1.4.1: rtx_debug_scan_rate (a diagnostic; no layout change).
  *  1.4.0: rtx_schedule.prio_bar1..3 (after prepass_cap_split, before
  *         `reserved`): dynamic lane-mode wave priority; the struct grew by
@@ -395,7 +397,13 @@ RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
  * 8-sphere block start_block % ceil(count / 8) and wrapping round — the
  * start the large-scene kernels take from their workgroup's position word
  * (DESIGN.md §3 "pack start"); the result is the in-order scan's for every
- * start (ties between spheres on either side of the wrap included). */
+ * start (ties between spheres on either side of the wrap included).
+ * start_block = RTX_DEBUG_CULLED: for a world of 64..512 spheres, the culled
+ * scan the render's lane mode runs on such scenes (a spatially ordered copy
+ * of the spheres whose 8-sphere blocks are skipped when no lane's line
+ * passes their bounding sphere, DESIGN.md §3 "culled scan"); other worlds
+ * scan from block RTX_DEBUG_CULLED % ceil(count / 8) as above. */
+#define RTX_DEBUG_CULLED 0xFFFFFFFFu
 RTX_API int rtx_debug_hit_world_from(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                      float t_min, float t_max, uint32_t start_block,
                                      float *out);

@@ -60,6 +60,9 @@ constexpr size_t kErrWord = 4;
 #ifndef RTX_FLAT
 #define RTX_FLAT 1
 #endif
+#ifndef RTX_CULL  // A/B build: 0 = no culled layout (the lane-mode scan visits every block)
+#define RTX_CULL 1
+#endif
 
 struct rtx_ctx {
     int device = 0;
@@ -72,6 +75,11 @@ struct rtx_ctx {
     float smag = 0.0f;
     float flat_cy = 0.0f;  // scene's flat run of `pre` blocks (rtx_internal.h KScene)
     uint32_t flat_lo = 0, flat_hi = 0;
+    // culled layout (rtx_internal.h KScene; none: null)
+    float *d_cpre = nullptr;
+    float *d_cbnd = nullptr;
+    uint32_t *d_cperm = nullptr;
+    uint32_t n_cpad = 0, cflat_lo = 0;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
@@ -139,6 +147,12 @@ void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_cen);
     (void)hipFree(c->d_mtype);
     (void)hipFree(c->d_mval);
+    (void)hipFree(c->d_cpre);
+    (void)hipFree(c->d_cbnd);
+    (void)hipFree(c->d_cperm);
+    c->d_cpre = c->d_cbnd = nullptr;
+    c->d_cperm = nullptr;
+    c->n_cpad = c->cflat_lo = 0;
     c->d_soa = nullptr;
     c->d_pre = nullptr;
     c->d_pre4 = nullptr;
@@ -162,6 +176,11 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.mval = c->d_mval;
     s.n = c->n;
     s.n_pad = c->n_pad;
+    s.cpre = c->d_cpre;
+    s.cbnd = c->d_cbnd;
+    s.cperm = c->d_cperm;
+    s.n_cpad = c->n_cpad;
+    s.cflat_lo = c->cflat_lo;
     return s;
 }
 
@@ -431,6 +450,84 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
     return RTX_OK;
 }
 
+// The culled layout (rtx_internal.h KScene, rtx_prefilter.h cull_bound):
+// sections of spheres — large ones (r > 8x the median), the other non-flat
+// ones, the flat ones (height flat_cy, when the scene has a flat run) — each
+// in Morton order of its centres (x, z for the flat section; x, y, z
+// otherwise) and padded to whole blocks with copies of its last sphere whose
+// prefilter R is -inf: never flagged (Q = -inf), except by a lane outside the
+// prefilter's safe region (thr = -inf flags everything), which then resolves
+// the copy to the same key as the sphere itself — no result changes either way.
+struct CullLayout {
+    std::vector<float> pre, bnd;
+    std::vector<uint32_t> perm;
+    std::vector<uint8_t> pad;  // position holds a padding copy
+    uint32_t flat_lo = 0;
+};
+static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4, bool has_flat, float flat_cy) {
+    const uint32_t n = w->count;
+    const float *S = w->spheres;
+    std::vector<float> rs(n);
+    for (uint32_t i = 0; i < n; ++i) rs[i] = std::fabs(S[4 * i + 3]);
+    std::nth_element(rs.begin(), rs.begin() + n / 2, rs.end());
+    const float big = 8.0f * rs[n / 2];
+    std::vector<uint32_t> sec[3];
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool fl = has_flat && __builtin_bit_cast(uint32_t, S[4 * i + 1]) == __builtin_bit_cast(uint32_t, flat_cy);
+        sec[std::fabs(S[4 * i + 3]) > big ? 0 : fl ? 2 : 1].push_back(i);
+    }
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], (double)S[4 * i + k]), hi[k] = std::max(hi[k], (double)S[4 * i + k]);
+    auto q = [&](uint32_t i, int k) -> uint64_t {
+        const double span = hi[k] - lo[k];
+        return span > 0.0 ? (uint64_t)std::min(1023.0, std::floor(((double)S[4 * i + k] - lo[k]) / span * 1024.0)) : 0;
+    };
+    auto morton = [&](uint32_t i, bool flat) {
+        uint64_t key = 0;
+        for (int bit = 0; bit < 10; ++bit) {
+            if (flat)
+                key |= ((q(i, 0) >> bit) & 1u) << (2 * bit) | ((q(i, 2) >> bit) & 1u) << (2 * bit + 1);
+            else
+                key |= ((q(i, 0) >> bit) & 1u) << (3 * bit) | ((q(i, 1) >> bit) & 1u) << (3 * bit + 1) |
+                       ((q(i, 2) >> bit) & 1u) << (3 * bit + 2);
+        }
+        return key;
+    };
+    CullLayout L;
+    for (int k = 0; k < 3; ++k) {
+        if (sec[k].empty()) continue;
+        std::stable_sort(sec[k].begin(), sec[k].end(),
+                         [&](uint32_t a, uint32_t b) { return morton(a, k == 2) < morton(b, k == 2); });
+        if (k == 2) L.flat_lo = (uint32_t)L.perm.size() / 8;
+        for (uint32_t i : sec[k]) L.perm.push_back(i), L.pad.push_back(0);
+        while (L.perm.size() % 8) L.perm.push_back(sec[k].back()), L.pad.push_back(1);
+    }
+    if (sec[2].empty()) L.flat_lo = (uint32_t)L.perm.size() / 8;
+    const uint32_t np = (uint32_t)L.perm.size(), nblk = np / 8, ngrp = (nblk + 7) / 8;
+    L.pre.assign(4 * (size_t)np, 0.0f);
+    for (uint32_t p = 0; p < np; ++p) {
+        const float4 v = pre4[L.perm[p]];
+        float *blk = &L.pre[32 * (size_t)(p / 8)];
+        blk[p % 8] = v.x, blk[8 + p % 8] = v.y, blk[16 + p % 8] = v.z, blk[24 + p % 8] = L.pad[p] ? -INFINITY : v.w;
+    }
+    L.bnd.assign(32 * (size_t)ngrp, 0.0f);
+    for (uint32_t g = 0; g < ngrp; ++g)
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t b = 8 * g + j;
+            float *gb = &L.bnd[32 * (size_t)g];
+            if (b >= nblk) {  // past the last block: masked off by the kernel; flat height for a flat group
+                gb[8 + j] = 8 * g >= L.flat_lo ? flat_cy : 0.0f;
+                continue;
+            }
+            const float *sp[8];
+            for (int i = 0; i < 8; ++i) sp[i] = &S[4 * (size_t)L.perm[8 * b + i]];
+            const rtx::CullBound cb = rtx::cull_bound(sp, 8, b >= L.flat_lo, flat_cy);
+            gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
+        }
+    return L;
+}
+
 int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (!c || !w) return fail(RTX_ERR_INVALID, "rtx_upload_world: null argument");
     if (w->reserved != 0) return fail(RTX_ERR_INVALID, "rtx_upload_world: reserved must be 0");
@@ -511,6 +608,9 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         mval[i] = make_float4(w->mat_values[4 * i + 0], w->mat_values[4 * i + 1],
                               w->mat_values[4 * i + 2], w->mat_values[4 * i + 3]);
     }
+    CullLayout cl;
+    const bool cull = RTX_CULL && n >= rtx::kCullMinN && n <= rtx::kCullMaxN;
+    if (cull) cl = build_cull(w, pre4, flat_hi > flat_lo, flat_cy);
     RTX_HIP(hipStreamSynchronize(c->stream));
     free_world(c);
     const size_t cap = n ? n : 1;
@@ -530,6 +630,18 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         RTX_HIP(hipMemcpyAsync(c->d_mtype, mtype.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_mval, mval.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipStreamSynchronize(c->stream));
+    }
+    if (cull) {
+        RTX_HIP(hipMalloc(&c->d_cpre, cl.pre.size() * sizeof(float)));
+        RTX_HIP(hipMalloc(&c->d_cbnd, cl.bnd.size() * sizeof(float)));
+        RTX_HIP(hipMalloc(&c->d_cperm, cl.perm.size() * sizeof(uint32_t)));
+        RTX_HIP(hipMemcpyAsync(c->d_cpre, cl.pre.data(), cl.pre.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_cbnd, cl.bnd.data(), cl.bnd.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        RTX_HIP(hipMemcpyAsync(c->d_cperm, cl.perm.data(), cl.perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               c->stream));
+        RTX_HIP(hipStreamSynchronize(c->stream));
+        c->n_cpad = (uint32_t)cl.perm.size();
+        c->cflat_lo = cl.flat_lo;
     }
     if (c->n != n) c->n_changed = true;
     c->n = n;

@@ -2,7 +2,8 @@
 // only by the Makefile's variant builds (prof: per-section clock sums and
 // scan/resolve event counts, tools/section_prof.py; ptime: per-pixel start /
 // end times, tools/pixel_timeline.py; cprof: per-section clocks of tier-1
-// coop segments, tools/coop_prof.py). In the product build every hook below
+// coop segments, tools/coop_prof.py; rays: a sample of lane-mode wave
+// iterations' rays, tools/ray_sample.py). In the product build every hook below
 // is empty and the per-wave Diag state has no members, so the hot loops'
 // text carries one call per hook and no diagnostic code.
 #pragma once
@@ -18,6 +19,9 @@
 #ifndef RTX_DIAG_COOP  // per-section clocks of tier-N (N = its value) coop segments into wave_times[0..7]
 #define RTX_DIAG_COOP 0
 #endif
+#ifndef RTX_DIAG_RAYS  // every RTX_DIAG_RAYS-th lane-mode wave iteration's rays into wave_times
+#define RTX_DIAG_RAYS 0
+#endif
 
 namespace rtx {
 namespace {
@@ -25,7 +29,9 @@ namespace {
 #if RTX_DIAG_PROF
 // Event counters, one set per wave in LDS: [0] blocks scanned [1] blocks
 // recorded (some lane had a candidate) [2] resolve iterations [3] lanes
-// falling back to the in-order scan [4] candidate entries (lanes)
+// falling back to the in-order scan [4] candidate entries (lanes) [5] candidate
+// spheres (the resolve's work, summed over the wave's lanes) [6] blocks of the
+// culled scan whose bound some lane passed
 __device__ __forceinline__ uint32_t *diag_slots() {
     __shared__ uint32_t s[4][8];
     return s[(threadIdx.x / 64) & 3u];
@@ -54,6 +60,9 @@ __device__ __forceinline__ void diag_add(int k, uint32_t v) {
 // [0] ray exchange + line setup [1] scan + resolve [2] reduction [3] shade
 // [4] loop between segments [5] segments).
 struct Diag {
+#if RTX_DIAG_RAYS
+    uint32_t rit = 0;
+#endif
 #if RTX_DIAG_PROF
     unsigned long long pr[7] = {0, 0, 0, 0, 0, 0, 0};
     unsigned long long tq = 0;
@@ -125,12 +134,38 @@ struct Diag {
         (void)tier;
 #endif
     }
+    // rays (RTX_DIAG_RAYS): a sampled lane-mode iteration appends one record
+    // of 64 lanes x 4 words (o.x o.y | o.z d.x | d.y d.z | live, slot) at
+    // wave_times[64 + 256 * r], r = wave_times[0]++ (records past the buffer
+    // are dropped). Called wave-uniformly.
+    __device__ __forceinline__ void rays(const KParams &P, f3 o, f3 d, bool live, uint32_t slot) {
+#if RTX_DIAG_RAYS
+        if (!P.wave_times) return;
+        const uint32_t w = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+        if ((++rit + w * 13u) % (uint32_t)RTX_DIAG_RAYS != 0u) return;
+        unsigned long long r = 0;
+        if ((threadIdx.x & 63u) == 0u) r = atomicAdd(&P.wave_times[0], 1ull);
+        r = __shfl(r, 0, 64);
+        const unsigned long long base = 64ull + 256ull * r;
+        if (base + 256ull > 2ull * P.wave_cap) return;
+        auto pk = [](float a, float b) {
+            return ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
+        };
+        unsigned long long *q = P.wave_times + base + 4u * (threadIdx.x & 63u);
+        q[0] = pk(o.x, o.y);
+        q[1] = pk(o.z, d.x);
+        q[2] = pk(d.y, d.z);
+        q[3] = ((unsigned long long)slot << 32) | (live ? 1u : 0u);
+#else
+        (void)P, (void)o, (void)d, (void)live, (void)slot;
+#endif
+    }
     // the wave's sums into P.wave_times
     __device__ __forceinline__ void finish(const KParams &P) {
 #if RTX_DIAG_PROF
         if (P.wave_times && (threadIdx.x & 63u) == 0u) {
             for (int k = 0; k < 7; ++k) atomicAdd(&P.wave_times[k], pr[k]);
-            for (int k = 0; k < 5; ++k) atomicAdd(&P.wave_times[8 + k], (unsigned long long)diag_slots()[k]);
+            for (int k = 0; k < 7; ++k) atomicAdd(&P.wave_times[8 + k], (unsigned long long)diag_slots()[k]);
         }
 #endif
 #if RTX_DIAG_COOP
@@ -159,7 +194,7 @@ __device__ __forceinline__ void diag_pixel_end(const KParams &P, uint32_t gid) {
     (void)gid;
 #endif
 }
-constexpr bool kDiagAny = RTX_DIAG_PROF || RTX_DIAG_PIXEL || RTX_DIAG_COOP;
+constexpr bool kDiagAny = RTX_DIAG_PROF || RTX_DIAG_PIXEL || RTX_DIAG_COOP || RTX_DIAG_RAYS;
 
 }  // namespace
 }  // namespace rtx

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "rtx_device_math.h"
@@ -645,18 +646,32 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
 // is loaded before the current one is tested, so a load from L2/HBM (cen,
 // large scenes) runs under the previous test (the order of tests is
 // unchanged; C5 -1.5 %, C2 neutral: DESIGN.md §7 R2z).
-template <typename Ld>
+// `gi(p)` maps a list position to the scene index (the culled layout's
+// position map; identity for `pre`).
+struct GiIdentity {
+    __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return p; }
+};
+template <typename Ld, typename Gi = GiIdentity>
 __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t *list, uint32_t m, f3 o, f3 d,
                                               float a, float inv_a, float t_min, float &best, int &idx,
-                                              uint32_t cap = (uint32_t)kCand) {
+                                              uint32_t cap = (uint32_t)kCand, Gi gi = Gi()) {
     bool ok = true;
     uint32_t j = 0;
     uint32_t e = list[threadIdx.x];  // entry 0 (unused when m == 0)
     RTX_DIAG_ADD(4, (uint32_t)__popcll(__ballot(m != 0u)));
+#if RTX_DIAG_PROF
+    {  // candidates of the wave (the resolve's rounds are their max over lanes)
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < m; ++q) c += (uint32_t)__popc(list[min(q, cap) * kRB + threadIdx.x] >> 24);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
+        RTX_DIAG_ADD(5, c);
+    }
+#endif
     // next candidate: sphere index i (live = the lane has one), then advance
     auto next = [&](uint32_t &i, bool &live) {
         live = j < m;
-        i = (e & 0xffffffu) + (uint32_t)__builtin_ctz(live ? (e >> 24) : 1u);
+        i = gi((e & 0xffffffu) + (uint32_t)__builtin_ctz(live ? (e >> 24) : 1u));
         e &= e - (1u << 24);  // drop that candidate from the mask
         const bool adv = live && (e >> 24) == 0u;
         j += adv ? 1u : 0u;
@@ -686,6 +701,129 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
                                             uint32_t m, f3 o, f3 d, float a, float inv_a, float t_min,
                                             float &best, int &idx) {
     return resolve_pre_t([cen](uint32_t i) { return cen[i]; }, n, list, m, o, d, a, inv_a, t_min, best, idx);
+}
+
+// The culled scan (KScene::cpre / cbnd, small scenes; DESIGN.md §3 "culled
+// scan"): blocks [b, n_cpad / 8) of the spatially ordered layout, in groups
+// of 8. A group's 8 block bounds are tested like 8 spheres (the same 7/5-op
+// test, against thr_b = thr * kCullThrScale: rtx_prefilter.h cull_bound), one
+// ballot per bound; only the blocks some lane's line passes are scanned, with
+// scan_range's per-block test and list entries (positions of the layout:
+// the resolve maps them through cperm). Returns the block to resume at: the
+// end, or the block after the one at which some lane's list filled (a resumed
+// group is tested again, its earlier blocks masked off). Wave-uniform.
+__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, uint32_t *list,
+                                                uint32_t &cnt) {
+    cnt = 0;
+    uint32_t *my = list + threadIdx.x;
+    const uint32_t nblk = S.n_cpad / 8u;
+    const LineFlat K = line_test_flat(T, S.flat_cy);
+    const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
+    const f2v th = {T.thr, T.thr};
+    const float thr_b = T.thr * kCullThrScale;
+    // Q of 4 pairs of spheres (or bounds) of an AoSoA-8 block. The block's
+    // floats are read first, all of them, so that they arrive by a few wide
+    // scalar loads and one wait (read at their use, the compiler split them
+    // into pair loads with a wait in the middle).
+    auto quad = [&](auto flat, cfloat_p blk, f2v *q) {
+        float v[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (!decltype(flat)::value || i < 8 || i >= 16) v[i] = blk[i];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const f2v cx = {v[2 * p], v[2 * p + 1]};
+            const f2v cz = {v[16 + 2 * p], v[17 + 2 * p]};
+            const f2v R = {v[24 + 2 * p], v[25 + 2 * p]};
+            f2v pu, pv;
+            if constexpr (decltype(flat)::value) {
+                pu = fma2(cx, ux, fma2(cz, uz, ku));
+                pv = fma2(cz, vz, kv);
+            } else {
+                const f2v cy = {v[8 + 2 * p], v[9 + 2 * p]};
+                pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+                pv = fma2(cy, vy, fma2(cz, vz, nov));
+            }
+            q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+        }
+    };
+    // one block of spheres: scan_range's finish (ballot, list entry)
+    auto step = [&](auto flat, uint32_t bb) -> bool {
+        f2v q[4];
+        quad(flat, (cfloat_p)S.cpre + 32u * bb, q);
+        const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
+                                             q[2].y), q[3].x), q[3].y);
+        RTX_DIAG_ADD(0, 1u);
+        if (__ballot(!(mx < T.thr)) != 0ull) {
+            RTX_DIAG_ADD(1, 1u);
+            uint32_t inv = 0;
+#pragma unroll
+            for (int p = 3; p >= 0; --p) {
+                const f2v sq = q[p] - th;
+                inv = (inv << 1) | (__float_as_uint(sq.y) >> 31);
+                inv = (inv << 1) | (__float_as_uint(sq.x) >> 31);
+            }
+            const uint32_t mask = ~inv & 0xffu;
+            my[cnt * kRB] = (8u * bb) | (mask << 24);
+            cnt += mask != 0u ? 1u : 0u;
+            return __ballot(cnt == (uint32_t)kCand) != 0ull;
+        }
+        return false;
+    };
+    using Flat = std::integral_constant<bool, true>;
+    using Full = std::integral_constant<bool, false>;
+    while (b < nblk) {
+        const uint32_t g = b >> 3;
+        f2v q[4];
+        if (8u * g >= S.cflat_lo)
+            quad(Flat(), (cfloat_p)S.cbnd + 32u * g, q);
+        else
+            quad(Full(), (cfloat_p)S.cbnd + 32u * g, q);
+        uint32_t m = 0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            m |= (__ballot(!(q[p].x < thr_b)) != 0ull ? 1u : 0u) << (2 * p);
+            m |= (__ballot(!(q[p].y < thr_b)) != 0ull ? 1u : 0u) << (2 * p + 1);
+        }
+        const uint32_t left = nblk - 8u * g;
+        m &= (left >= 8u ? 0xffu : (1u << left) - 1u) & (0xffu << (b & 7u));
+        RTX_DIAG_ADD(6, (uint32_t)__popc(m));
+        while (m != 0u) {
+            const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            if (bb >= S.cflat_lo ? step(Flat(), bb) : step(Full(), bb)) return bb + 1u;
+        }
+        b = 8u * g + 8u;
+    }
+    return nblk;
+}
+
+// hit_world over the culled layout: same (best, idx) as hit_world_pre (the
+// resolution rule is order-independent; the bounds never drop a reference
+// candidate). ld(i): (centre, radius) of scene sphere i; gi(p): the scene
+// index at layout position p < n_cpad.
+template <typename Ld, typename Gi>
+__device__ __forceinline__ int hit_world_culled(const KScene &S, Ld ld, Gi gi, f3 o, f3 d, float a, float inv_a,
+                                                float t_min, float &best, uint32_t *list) {
+    const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    const float best0 = best;
+    int idx = -1;
+    bool ok = true;
+    const uint32_t nblk = S.n_cpad / 8u, last = S.n_cpad - 1u;
+    auto gclamp = [gi, last](uint32_t p) { return gi(min(p, last)); };
+    uint32_t b = 0;
+    do {
+        uint32_t cnt;
+        b = scan_culled(S, b, T, list, cnt);
+        ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, (uint32_t)kCand, gclamp) && ok;
+    } while (b < nblk);
+    if (!ok) {
+        RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
+        best = best0;
+        idx = hit_blocks_seq((cfloat_p)S.soa, S.n_pad / 8, 0, o, d, a, inv_a, t_min, best, -1);
+    }
+    return idx;
 }
 
 // hit_world with the prefiltered scan: same (best, idx) as the in-order
@@ -780,11 +918,16 @@ __host__ __device__ constexpr uint32_t coop_lds_bytes(uint32_t n) {
     return coop_npad(n) * 4u * (uint32_t)sizeof(float) + n * (uint32_t)sizeof(float);
 }
 static_assert(coop_lds_bytes(kCoopLds) <= 12800, "LDS copy of the scene: 5 render blocks per CU");
+// ... plus the culled layout's position map (uint16, after the radii)
+__host__ __device__ constexpr uint32_t cull_lds_bytes(uint32_t n_cpad) { return (2u * n_cpad + 15u) / 16u * 16u; }
+static_assert(kCullMaxN <= kCoopLds && coop_lds_bytes(kCullMaxN) + cull_lds_bytes(kCullMaxN + 24u) <= 12800,
+              "the position map fits beside the LDS copy (3 sections padded: n_cpad <= n + 21)");
 
 struct SphLds {
     static constexpr bool kPadded = true;  // npairs is a multiple of 64: every group's steps stay inside
     const float *pr;   // [npairs][8]
     const float *rad;  // [n]
+    const uint16_t *perm;  // [n_cpad] the culled layout's position map (k_render with KScene::cpre), or unset
     uint32_t n, npairs;
     __device__ __forceinline__ void pair(uint32_t p, f2v &cx, f2v &cy, f2v &cz, f2v &R) const {
         const float4 *q = reinterpret_cast<const float4 *>(pr + 8u * p);
@@ -818,12 +961,18 @@ struct SphGlobal {
 // Build the block's LDS copy (all threads of the block; the caller
 // synchronises): sphere i < npad at pair i/2, slot i%2 (copies of n - 1
 // beyond n), radii after the pairs.
-__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on, uint32_t nthreads = kRB) {
+__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on, uint32_t nthreads = kRB,
+                                           bool with_perm = false) {
     SphLds l;
     l.n = S.n;
     l.npairs = coop_npad(S.n) / 2u;
     l.pr = base;
     l.rad = base + 8u * l.npairs;
+    l.perm = reinterpret_cast<const uint16_t *>(base + 8u * l.npairs + S.n);
+    if (on && with_perm && S.cpre) {
+        uint16_t *pm = const_cast<uint16_t *>(l.perm);
+        for (uint32_t i = threadIdx.x; i < S.n_cpad; i += nthreads) pm[i] = (uint16_t)S.cperm[i];
+    }
     if (on) {
         float *pr = base, *rad = base + 8u * l.npairs;
         for (uint32_t i = threadIdx.x; i < 2u * l.npairs; i += nthreads) {
@@ -1827,7 +1976,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
     (void)coop_ws;
     // the coop's sphere data: a block-wide LDS copy for small scenes (SphLds)
     const bool coop_lds = P.scene.n <= kCoopLds;
-    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds);
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds, kRB, !kPF);
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
@@ -1951,6 +2100,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
             set_prio(__ballot(L.active && L.slot < kh + P.prio_slots) != 0ull ? P.prio_hot : 0u);
         }
         bool promoted = false;
+        D.rays(P, L.o, L.d, L.active, L.slot);
         if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
             float best = __uint_as_float(0x7f800000u);
             auto ldc = [&P](uint32_t i) { return P.scene.cen[i]; };
@@ -1961,11 +2111,15 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
-            // from it (the same centre and radius floats as cen) instead of HBM/L2
-            const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
-                                ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
-                                                        L.a, L.inv_a, kTMin, best, list, nullptr, 0,
-                                                        RTX_SCAN_LDS ? sl.pr : nullptr)
+            // from it (the same centre and radius floats as cen) instead of
+            // HBM/L2; with a culled layout they scan it (scan_culled)
+            auto lds_sph = [sl](uint32_t i) { return sl.sphere(i); };
+            const int hit = (!kPF && coop_lds && P.scene.cpre)
+                                ? hit_world_culled(P.scene, lds_sph, [sl](uint32_t p) { return (uint32_t)sl.perm[p]; },
+                                                   L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                            : (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
+                                ? hit_world_pre_ld<kPF>(P.scene, lds_sph, L.o, L.d, L.a, L.inv_a, kTMin, best, list,
+                                                        nullptr, 0, RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
             promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
@@ -2558,7 +2712,7 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
     count_segments(P, L.segs);
     // diagnostic only (rtx_debug_wave_times, armed with 2 x waves): per wave
     // (start, end) s_memrealtime, then (shader clocks, segments) in the upper half
-    if (P.wave_times && lane == 0u && wave < P.wave_cap / 2) {
+    if (!RTX_DIAG_RAYS && P.wave_times && lane == 0u && wave < P.wave_cap / 2) {
         P.wave_times[2 * wave] = t_start;
         P.wave_times[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
         P.wave_times[P.wave_cap + 2 * wave] = __builtin_amdgcn_s_memtime() - c_start;
@@ -2605,7 +2759,9 @@ __global__ void __launch_bounds__(kBlock) k_unpermute(const float4 *__restrict__
 }
 
 // t_min > 0 and t_max >= t_min (rtx_debug_hit_world checks): the resolve
-// orders roots by their bits (hit_key).
+// orders roots by their bits (hit_key). start = kDebugCulled: the culled
+// scan (k_render's lane mode for scenes with KScene::cpre), when the scene has it.
+constexpr uint32_t kDebugCulled = 0xffffffffu;
 __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const float *rays,
                                                             uint32_t nrays, float t_min,
                                                             float t_max, uint32_t start, float *out) {
@@ -2619,8 +2775,11 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     const float inv_a = 1.0f / a;
     float best = t_max;
     const int idx =
-        min((S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
-                                  : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)),
+        min((start == kDebugCulled && S.cpre)
+                ? hit_world_culled(S, [&S](uint32_t j) { return S.cen[min(j, S.n - 1u)]; },
+                                   [&S](uint32_t p) { return S.cperm[p]; }, o, d, a, inv_a, t_min, best, list)
+            : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
+                                   : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
     float *r = out + 10 * (size_t)i;
     if (idx < 0) {
@@ -2654,7 +2813,7 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
 __global__ void RTX_RENDER_BOUNDS k_debug_scan_rate(const KParams P, uint32_t reps, unsigned long long *sink) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kListBytes + kCoopBytes), true);
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kListBytes + kCoopBytes), true, kRB, true);
     __syncthreads();
     const uint32_t npix = P.rows_local * P.width;
     const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
@@ -2669,8 +2828,13 @@ __global__ void RTX_RENDER_BOUNDS k_debug_scan_rate(const KParams P, uint32_t re
     uint32_t acc = 0;
     for (uint32_t r = 0; r < reps; ++r) {
         float best = __uint_as_float(0x7f800000u);
-        const int hit = hit_world_pre_ld<false>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, o, d, a, inv_a,
-                                                kTMin, best, list, nullptr, 0, RTX_SCAN_LDS ? sl.pr : nullptr);
+        const int hit = P.scene.cpre
+                            ? hit_world_culled(P.scene, [sl](uint32_t i) { return sl.sphere(i); },
+                                               [sl](uint32_t p) { return (uint32_t)sl.perm[p]; }, o, d, a, inv_a,
+                                               kTMin, best, list)
+                            : hit_world_pre_ld<false>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, o, d, a,
+                                                      inv_a, kTMin, best, list, nullptr, 0,
+                                                      RTX_SCAN_LDS ? sl.pr : nullptr);
         acc += (uint32_t)hit ^ __float_as_uint(best);
     }
 #pragma unroll
@@ -2772,7 +2936,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() + 16 + kPfLdsBytes : kListBytes) + kCoopBytes +  // kPF: the pack word
-           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
+           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) + (s.cpre ? cull_lds_bytes(s.n_cpad) : 0u) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
@@ -3021,7 +3185,8 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
 hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
                                   hipStream_t stream) {
     if (p.scene.n > kCoopLds || use_pf(p.scene) || (uint64_t)p.rows_local * p.width == 0) return hipErrorInvalidValue;
-    const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n);
+    const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n) +
+                       (p.scene.cpre ? cull_lds_bytes(p.scene.n_cpad) : 0u);
     const uint32_t blocks = resident_blocks((const void *)k_debug_scan_rate, lds);
     *waves = blocks * (kRB / 64);
     hipLaunchKernelGGL(k_debug_scan_rate, dim3(blocks), dim3(kRB), lds, stream, p, reps, sink);

@@ -160,4 +160,60 @@ RTX_HD float line_test_q_flat(const LineTest &T, const LineFlat &K, float cx, fl
     return fmaf(-pv, pv, fmaf(-pu, pu, R));
 }
 
+// Block bounds of the culled scan (DESIGN.md §3 "culled scan"). The lane-
+// mode scan of small scenes visits 8-sphere blocks of a spatially ordered
+// copy of the scene and first tests, per lane, each block's bounding sphere
+// (C_b, R_b) with the same 7/5-op test as a sphere: a block no lane's line
+// passes is skipped. Exactness needs: reference disc_i >= 0 for a sphere i
+// of the block  ==>  the block test passes. Derivation (u = 2^-24, exact
+// reals unless fl()):
+//   reference disc_i >= 0  ==>  dperp_i^2 <= r_i^2 + u (13|oc_i|^2 + 7 r_i^2)
+//                          <= A_i + B,  A_i = r_i^2 (1 + 8u) + 27u |c_i|^2,
+//                                        B = 26u |o|^2         (|oc|^2 <= 2|o|^2 + 2|c|^2)
+//   dperp_b <= |c_i - C_b| + dperp_i <= rho + sqrt(B),  rho = max_i (|c_i - C_b| + sqrt(A_i))
+//   dperp_b^2 <= (1 + k) rho^2 + (1 + 1/k) B            (any k > 0; k = 1/32)
+// The block test is the sphere test on (C_b, R_b), whose own rounding the
+// sphere margins cover (above: u (53 S^2 + 11 R), S = |C_b| + |o|), so
+//   R_b   = fl_up((1 + k) rho^2 (1 + kPreMarginR) + kPreMarginC |C_b|^2 + kPreFloor)
+//   thr_b = -(kPreMarginO + (1 + 1/k) 26u) |o|^2 - kPreFloor  >=  thr * kCullThrScale
+// (kPreMarginO + 33 * 26u = 6.71e-5 <= 1.6e-5 * 4.25 = 6.8e-5; thr = -inf
+// stays -inf). tests/prefilter_check.cpp checks the claim on adversarial
+// near-tangent rays through random blocks.
+constexpr float kCullThrScale = 4.25f;
+constexpr double kCullK = 1.0 / 32.0;
+
+struct CullBound {
+    float cx, cy, cz, R;
+};
+// Spheres (cx, cy, cz, r)[m] as uploaded; flat: every centre has height
+// flat_cy (the bound's centre takes it exactly, so the 5-op test applies).
+inline CullBound cull_bound(const float *const *sph, int m, bool flat, float flat_cy) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < m; ++i)
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fmin(lo[k], (double)sph[i][k]);
+            hi[k] = fmax(hi[k], (double)sph[i][k]);
+        }
+    CullBound b;
+    b.cx = (float)(0.5 * (lo[0] + hi[0]));
+    b.cy = flat ? flat_cy : (float)(0.5 * (lo[1] + hi[1]));
+    b.cz = (float)(0.5 * (lo[2] + hi[2]));
+    const double u = 5.9604644775390625e-08;
+    double rho = 0.0;
+    for (int i = 0; i < m; ++i) {
+        const double dx = (double)sph[i][0] - b.cx, dy = (double)sph[i][1] - b.cy, dz = (double)sph[i][2] - b.cz;
+        const double r = sph[i][3];
+        const double c2 = (double)sph[i][0] * sph[i][0] + (double)sph[i][1] * sph[i][1] + (double)sph[i][2] * sph[i][2];
+        const double A = r * r * (1.0 + 8.0 * u) + 27.0 * u * c2;
+        // (double rounding of these few ops is ~1e-16 relative: the 1e-12 covers it)
+        rho = fmax(rho, (sqrt(dx * dx + dy * dy + dz * dz) + sqrt(A)) * (1.0 + 1e-12));
+    }
+    const double cb2 = (double)b.cx * b.cx + (double)b.cy * b.cy + (double)b.cz * b.cz;
+    const double R = (1.0 + kCullK) * rho * rho * (1.0 + kPreMarginR) + kPreMarginC * cb2 + (double)kPreFloor;
+    float f = (float)R;
+    if ((double)f < R) f = nextafterf(f, INFINITY);
+    b.R = f;
+    return b;
+}
+
 }  // namespace rtx

@@ -28,6 +28,7 @@ LIB_PATH = os.environ.get("RTX_LIB", os.path.join(_PKG_DIR, "lib", "librtx.so"))
 RTX_OK = 0
 RTX_ERR_INCOMPLETE = -5  # a render launch left pixels unwritten (ABI 1.3)
 SCHEDULE_ABI = 140  # the rtx_schedule layout this module passes (ABI 1.4.0)
+DEBUG_CULLED = 0xFFFFFFFF  # rtx_debug_hit_world_from: the culled scan (include/rtx.h RTX_DEBUG_CULLED)
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
@@ -420,7 +421,8 @@ class Context:
     def debug_hit_world(self, rays: np.ndarray, t_min: float = 0.001,
                         t_max: float = float("inf"), start_block: Optional[int] = None) -> np.ndarray:
         """hit_world on the GPU (rtx_debug_hit_world); start_block: the scan
-        starts at that 8-sphere block and wraps round (rtx_debug_hit_world_from)."""
+        starts at that 8-sphere block and wraps round (rtx_debug_hit_world_from);
+        DEBUG_CULLED: the culled scan (worlds of 64..512 spheres)."""
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
         out = np.zeros((rays.shape[0], 10), np.float32)
         if start_block is None:

@@ -40,6 +40,92 @@ static float ref_disc(const float o[3], const float d[3], const float c[3], floa
     return fmaf(hb, hb, -(a * cc));
 }
 
+// The culled scan's block bounds (rtx_prefilter.h cull_bound): a block of 8
+// spheres (a cluster of extent 1e-2..1e2 x the largest radius around a centre
+// of magnitude 1e-2..1e4, radii 1/8..1 x r, a third of the blocks flat: one
+// centre height), a near-tangent line to one of them; whenever the
+// reference's disc of that sphere is >= 0 (or NaN), the block test must pass
+// (line_test_q / line_test_q_flat on the bound against thr * kCullThrScale).
+static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
+    for (long k = 0; k < n; ++k) {
+        double cd[3], dir[3], e[3], t[3];
+        unit(cd);
+        const double cs = std::pow(10.0, -2.0 + 6.0 * uni());
+        const double r = std::pow(10.0, -3.0 + 5.0 * uni());
+        const double ext = r * std::pow(10.0, -2.0 + 4.0 * uni());
+        const bool flat = uni() < 0.33;
+        float sph[8][4];
+        for (int i = 0; i < 8; ++i) {
+            double off[3];
+            unit(off);
+            const double m = ext * uni();
+            for (int j = 0; j < 3; ++j) sph[i][j] = (float)(cs * cd[j] + m * off[j]);
+            if (flat) sph[i][1] = (float)(cs * cd[1]);
+            sph[i][3] = (float)(r * (0.125 + 0.875 * uni()));
+        }
+        const int j0 = (int)(uni() * 8.0) & 7;
+        const float *c = sph[j0];
+        const double rr = c[3];
+        unit(dir);
+        if (uni() < 0.05) {  // near the x axis
+            const double eps = std::pow(10.0, -8.0 + 6.0 * uni());
+            dir[1] = eps * sym(), dir[2] = eps * sym(), dir[0] = uni() < 0.5 ? -1.0 : 1.0;
+        }
+        const float *sp[8];
+        for (int i = 0; i < 8; ++i) sp[i] = sph[i];
+        const rtx::CullBound b = rtx::cull_bound(sp, 8, flat, sph[0][1]);
+        // half the lines graze the sphere on its side away from the bound's
+        // centre (the tightest case for the bound), the others at random
+        const double away[3] = {c[0] - (double)b.cx, c[1] - (double)b.cy, c[2] - (double)b.cz};
+        const double al = std::sqrt(away[0] * away[0] + away[1] * away[1] + away[2] * away[2]);
+        if (uni() < 0.5 && al > 0.0) {
+            for (int i = 0; i < 3; ++i) t[i] = away[i] / al;
+        } else {
+            unit(t);
+        }
+        const double td = t[0] * dir[0] + t[1] * dir[1] + t[2] * dir[2];
+        const double dn = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+        for (int i = 0; i < 3; ++i) e[i] = t[i] - td / dn * dir[i];
+        const double en = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        if (en < 1e-9) continue;
+        for (int i = 0; i < 3; ++i) e[i] /= en;
+        const double delta = std::pow(10.0, -9.0 + 8.0 * uni()) * (uni() < 0.5 ? -1.0 : 1.0);
+        const double dist = uni() < 0.8 ? rr * (1.0 + delta) : 3.0 * rr * uni();
+        const double along = sym() * std::pow(10.0, -1.0 + 4.0 * uni()) * std::fmax(ext + rr, 1.0);
+        const double dlen = std::pow(10.0, -3.0 + 6.0 * uni());
+        float o[3], d[3];
+        for (int i = 0; i < 3; ++i) {
+            o[i] = (float)(c[i] + dist * e[i] - along * dir[i]);
+            d[i] = (float)(dlen * dir[i]);
+        }
+        const float r2 = c[3] * c[3];
+        const float a = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
+        double sm = 0.0;
+        for (int i = 0; i < 8; ++i)
+            sm = std::fmax(sm, std::sqrt((double)sph[i][0] * sph[i][0] + (double)sph[i][1] * sph[i][1] +
+                                         (double)sph[i][2] * sph[i][2]) + sph[i][3]);
+        float smag = (float)sm;
+        if ((double)smag < sm) smag = std::nextafter(smag, INFINITY);
+        for (int j = 0; j < 3; ++j) rtx::pf_host_ulp[j] = (int)(uni() * 3.0) - 1;
+        const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
+        const float thr_b = T.thr * rtx::kCullThrScale;
+        const float q = flat ? rtx::line_test_q_flat(T, rtx::line_test_flat(T, b.cy), b.cx, b.cz, b.R)
+                             : rtx::line_test_q(T, b.cx, b.cy, b.cz, b.R);
+        const bool ref = !(ref_disc(o, d, c, -r2, a) < 0.0f);
+        ref_pos += ref;
+        if (ref && q < thr_b) {
+            if (++missed <= 5)
+                std::fprintf(stderr, "BLOCK MISS c=(%.9g %.9g %.9g) r=%.9g o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) q=%.9g thr_b=%.9g\n",
+                             c[0], c[1], c[2], c[3], o[0], o[1], o[2], d[0], d[1], d[2], q, thr_b);
+        }
+        if (ref && T.thr != -INFINITY) {
+            // the line's estimated dperp_b^2 against the bound's inflated R_b - thr_b
+            const double used = ((double)b.R - q) / ((double)b.R - thr_b);
+            if (used > max_used) max_used = used;
+        }
+    }
+}
+
 int main(int argc, char **argv) {
     const long n = argc > 1 ? std::atol(argv[1]) : 2000000;
     long ref_pos = 0, flagged = 0, missed = 0, unsafe = 0, false_pos = 0;
@@ -119,8 +205,12 @@ int main(int argc, char **argv) {
             if (used > max_used) max_used = used;
         }
     }
+    long b_ref = 0, b_missed = 0;
+    double b_used = -1e300;
+    block_cases(n / 2, b_ref, b_missed, b_used);
     std::printf("{\"cases\": %ld, \"reference_candidates\": %ld, \"flagged\": %ld, \"false_positives\": %ld, "
-                "\"unsafe_lanes\": %ld, \"missed\": %ld, \"max_margin_used\": %.6g}\n",
-                n, ref_pos, flagged, false_pos, unsafe, missed, max_used);
-    return missed ? 1 : 0;
+                "\"unsafe_lanes\": %ld, \"missed\": %ld, \"max_margin_used\": %.6g, \"block_cases\": %ld, "
+                "\"block_reference_candidates\": %ld, \"block_missed\": %ld, \"block_max_used\": %.9g}\n",
+                n, ref_pos, flagged, false_pos, unsafe, missed, max_used, n / 2, b_ref, b_missed, b_used);
+    return missed || b_missed ? 1 : 0;
 }

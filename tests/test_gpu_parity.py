@@ -172,21 +172,59 @@ def test_hit_world_wrapped_scan_starts(gpu_ctx, oracle, rtx, which):
         assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
 
 
-def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx):
+@pytest.mark.parametrize("scan", ["plain", "culled"])
+def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx, scan):
     """Rays whose line passes within 1e-9..1e-2 (relative) of a sphere's
     silhouette, on either side, plus near-vertical rays and rays near the x
     axis (the prefilter basis's degenerate direction), tiny and huge
     direction lengths (some outside the prefilter's safe range) and origins
     far down the line: the kernel's prefiltered scan (rtx_prefilter.h) must
-    return the reference scan's records bit for bit."""
+    return the reference scan's records bit for bit — the plain scan and the
+    culled one (block bounds first, spatial order, position map)."""
     rng = np.random.default_rng(11)
     world = rtx.random_world(11, depth=1, spp=1)
     rays = grazing_rays(world.spheres, 30000, rng, xaxis_frac=0.05)
     gpu_ctx.upload_world(world)
-    got = gpu_ctx.debug_hit_world(rays)
+    got = gpu_ctx.debug_hit_world(rays, start_block=rtx.DEBUG_CULLED if scan == "culled" else None)
     want = oracle.hit_world_f32(world, rays)
-    assert_bits_equal(got, want, "grazing rays")
+    assert_bits_equal(got, want, f"grazing rays, {scan} scan")
     assert (want[:, 0] == 1).mean() > 0.3
+
+
+@pytest.mark.parametrize("n", [64, 65, 130, 333, 486, 512])
+def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
+    """The culled scan (DESIGN.md §3 "culled scan") on scenes across its size
+    range: random spheres at mixed heights, a flat run at one height (the 5-op
+    bound test), a few large spheres (their own section) and duplicated
+    spheres whose ties must still go to the later index though the layout
+    reorders them; rays aimed at spheres, random ones and grazing ones, with
+    t_min's near the tie roots."""
+    rng = np.random.default_rng(n)
+    k = n // 3
+    flat = np.concatenate([rng.uniform(-11, 11, (k, 1)), np.full((k, 1), 0.2), rng.uniform(-11, 11, (k, 1)),
+                           np.full((k, 1), 0.2)], 1)
+    big = np.array([[0, -1000, 0, 1000], [0, 1, 0, 1.0], [-4, 1, 0, 1.0], [4, 1, 0, 1.0]])
+    m = n - k - len(big) - 8
+    other = np.concatenate([rng.uniform(-11, 11, (m, 1)), rng.uniform(0, 3, (m, 1)), rng.uniform(-11, 11, (m, 1)),
+                            rng.uniform(0.1, 0.5, (m, 1))], 1)
+    sph = np.concatenate([big[:1], other, flat, big[1:]]).astype(np.float32)
+    dup_src = rng.choice(len(sph) - 1, 8, replace=False) + 1
+    sph = np.concatenate([sph, sph[dup_src]]).astype(np.float32)  # the copies come later: they win ties
+    assert len(sph) == n
+    world = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
+    gpu_ctx.upload_world(world)
+    o = rng.uniform(-14, 14, (6000, 3)) + np.array([0, 8, 0])
+    d = (sph[rng.integers(1, n, 6000), :3] - o) + rng.normal(scale=0.15, size=(6000, 3))
+    rays = np.concatenate([np.concatenate([o, d], 1), grazing_rays(sph, 6000, rng, xaxis_frac=0.05),
+                           np.concatenate([rng.uniform(-12, 12, (3000, 3)), rng.normal(size=(3000, 3))], 1)])
+    rays = rays.astype(np.float32)
+    for t_min in (0.001, 0.5):
+        want = oracle.hit_world_f32(world, rays, t_min)
+        got = gpu_ctx.debug_hit_world(rays, t_min=t_min, start_block=rtx.DEBUG_CULLED)
+        assert_bits_equal(got, want, f"n={n} culled scan, t_min={t_min}")
+        hit = want[:, 9] >= 0
+        assert hit.mean() > 0.3
+        assert not np.isin(want[hit, 9], dup_src).any(), "a tie must go to the later duplicate"
 
 
 # ---------------------------------------------------------------------------

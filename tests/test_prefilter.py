@@ -6,8 +6,10 @@ cheaper, inflated line-distance test, and resolves every flagged sphere with
 the reference's own operations. The result is bit-identical only if the
 prefilter flags every sphere whose reference fp32 discriminant is >= 0 (or
 NaN). tests/prefilter_check.cpp evaluates both, with the header's own code,
-on adversarial near-tangent cases and must find no miss; the GPU side of the
-same claim is test_gpu_parity.py::test_hit_world_grazing_rays.
+on adversarial near-tangent cases and must find no miss; likewise for the
+culled scan's block bounds (a block is skipped only if no lane's line passes
+its bound). The GPU side of the same claims is
+test_gpu_parity.py::test_hit_world_grazing_rays (both scans).
 """
 import json
 import os
@@ -26,3 +28,8 @@ def test_prefilter_never_drops_a_reference_candidate(tmp_path):
     assert rep["reference_candidates"] > 1_000_000  # the near-tangent set is exercised
     # the rounding errors use a small share of the margin (rigorous bound: <= 0.38)
     assert rep["max_margin_used"] < 0.38, rep
+    # the culled scan's block bounds (rtx_prefilter.h cull_bound): no reference
+    # candidate's block is skipped; the tightest lines use the geometric part
+    # of R_b, 1 / (1 + k) = 0.97 of it, never the rounding margins
+    assert rep["block_missed"] == 0 and rep["block_reference_candidates"] > 500_000, rep
+    assert rep["block_max_used"] < 0.98, rep

@@ -54,4 +54,10 @@ for path in libs:
     rep["resolve_iters_per_iter"] = round(v[10] / seg_iters, 3)
     rep["fallback_lanes"] = int(v[11])
     rep["lanes_with_candidates_per_iter"] = round(v[12] / seg_iters, 2)
+    # candidate spheres per wave-iteration: the resolve's rounds are their max over the lanes
+    # (resolve_iters_per_iter); / 64 their mean per lane — the rounds a wave-wide compaction would take
+    rep["candidates_per_iter"] = round(v[13] / seg_iters, 2)
+    rep["compacted_rounds_per_iter"] = round(v[13] / seg_iters / 64.0, 3)
+    # culled scan: blocks whose bound some lane's line passed (they are scanned; the others skipped)
+    rep["cull_pass_blocks_per_iter"] = round(v[14] / seg_iters, 2)
     print(json.dumps(rep), flush=True)
