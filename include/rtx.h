@@ -398,11 +398,12 @@ RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
  * start the large-scene kernels take from their workgroup's position word
  * (DESIGN.md §3 "pack start"); the result is the in-order scan's for every
  * start (ties between spheres on either side of the wrap included).
- * start_block = RTX_DEBUG_CULLED: for a world of 64..512 spheres, the culled
- * scan the render's lane mode runs on such scenes (a spatially ordered copy
- * of the spheres whose 8-sphere blocks are skipped when no lane's line
- * passes their bounding sphere, DESIGN.md §3 "culled scan"); other worlds
- * scan from block RTX_DEBUG_CULLED % ceil(count / 8) as above. */
+ * start_block = RTX_DEBUG_CULLED: for a world of more than 1,024 spheres
+ * (after padding to 8), the culled scan the render's lane mode runs on such
+ * scenes (a spatially ordered copy of the spheres whose 8-sphere blocks are
+ * skipped when no lane's line passes their bounding sphere, DESIGN.md §3e
+ * "culled scan"); smaller worlds scan from block
+ * RTX_DEBUG_CULLED % ceil(count / 8) as above. */
 #define RTX_DEBUG_CULLED 0xFFFFFFFFu
 RTX_API int rtx_debug_hit_world_from(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                      float t_min, float t_max, uint32_t start_block,

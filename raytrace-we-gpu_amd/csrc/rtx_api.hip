@@ -60,9 +60,6 @@ constexpr size_t kErrWord = 4;
 #ifndef RTX_FLAT
 #define RTX_FLAT 1
 #endif
-#ifndef RTX_CULL  // A/B build: 0 = no culled layout (the lane-mode scan visits every block)
-#define RTX_CULL 1
-#endif
 
 struct rtx_ctx {
     int device = 0;
@@ -78,7 +75,9 @@ struct rtx_ctx {
     // culled layout (rtx_internal.h KScene; none: null)
     float *d_cpre = nullptr;
     float *d_cbnd = nullptr;
+    float *d_cbnd2 = nullptr;
     uint32_t *d_cperm = nullptr;
+    float4 *d_ccen = nullptr;
     uint32_t n_cpad = 0, cflat_lo = 0;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
@@ -149,9 +148,12 @@ void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_mval);
     (void)hipFree(c->d_cpre);
     (void)hipFree(c->d_cbnd);
+    (void)hipFree(c->d_cbnd2);
     (void)hipFree(c->d_cperm);
-    c->d_cpre = c->d_cbnd = nullptr;
+    (void)hipFree(c->d_ccen);
+    c->d_cpre = c->d_cbnd = c->d_cbnd2 = nullptr;
     c->d_cperm = nullptr;
+    c->d_ccen = nullptr;
     c->n_cpad = c->cflat_lo = 0;
     c->d_soa = nullptr;
     c->d_pre = nullptr;
@@ -178,7 +180,9 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.n_pad = c->n_pad;
     s.cpre = c->d_cpre;
     s.cbnd = c->d_cbnd;
+    s.cbnd2 = c->d_cbnd2;
     s.cperm = c->d_cperm;
+    s.ccen = c->d_ccen;
     s.n_cpad = c->n_cpad;
     s.cflat_lo = c->cflat_lo;
     return s;
@@ -459,7 +463,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
 // prefilter's safe region (thr = -inf flags everything), which then resolves
 // the copy to the same key as the sphere itself — no result changes either way.
 struct CullLayout {
-    std::vector<float> pre, bnd;
+    std::vector<float> pre, bnd, bnd2;
     std::vector<uint32_t> perm;
     std::vector<uint8_t> pad;  // position holds a padding copy
     uint32_t flat_lo = 0;
@@ -523,6 +527,23 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
             const float *sp[8];
             for (int i = 0; i < 8; ++i) sp[i] = &S[4 * (size_t)L.perm[8 * b + i]];
             const rtx::CullBound cb = rtx::cull_bound(sp, 8, b >= L.flat_lo, flat_cy);
+            gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
+        }
+    // the top level: one bound over each group's 64 spheres, 8 groups per super-group
+    const uint32_t nsg = (ngrp + 7) / 8;
+    L.bnd2.assign(32 * (size_t)nsg, 0.0f);
+    std::vector<const float *> sp64;
+    for (uint32_t s = 0; s < nsg; ++s)
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t g = 8 * s + j;
+            float *gb = &L.bnd2[32 * (size_t)s];
+            if (g >= ngrp) {
+                gb[8 + j] = 64 * s >= L.flat_lo ? flat_cy : 0.0f;
+                continue;
+            }
+            sp64.clear();
+            for (uint32_t p = 64 * g; p < std::min(64 * g + 64, np); ++p) sp64.push_back(&S[4 * (size_t)L.perm[p]]);
+            const rtx::CullBound cb = rtx::cull_bound(sp64.data(), (int)sp64.size(), 8 * g >= L.flat_lo, flat_cy);
             gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
         }
     return L;
@@ -609,7 +630,7 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
                               w->mat_values[4 * i + 2], w->mat_values[4 * i + 3]);
     }
     CullLayout cl;
-    const bool cull = RTX_CULL && n >= rtx::kCullMinN && n <= rtx::kCullMaxN;
+    const bool cull = RTX_CULL && n_pad > rtx::kScanPfMin;  // the large-scene (kPF) kernels scan it
     if (cull) cl = build_cull(w, pre4, flat_hi > flat_lo, flat_cy);
     RTX_HIP(hipStreamSynchronize(c->stream));
     free_world(c);
@@ -634,7 +655,14 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     if (cull) {
         RTX_HIP(hipMalloc(&c->d_cpre, cl.pre.size() * sizeof(float)));
         RTX_HIP(hipMalloc(&c->d_cbnd, cl.bnd.size() * sizeof(float)));
+        RTX_HIP(hipMalloc(&c->d_cbnd2, cl.bnd2.size() * sizeof(float)));
+        RTX_HIP(hipMemcpyAsync(c->d_cbnd2, cl.bnd2.data(), cl.bnd2.size() * sizeof(float), hipMemcpyHostToDevice,
+                               c->stream));
         RTX_HIP(hipMalloc(&c->d_cperm, cl.perm.size() * sizeof(uint32_t)));
+        RTX_HIP(hipMalloc(&c->d_ccen, cl.perm.size() * sizeof(float4)));
+        std::vector<float4> ccen(cl.perm.size());
+        for (size_t p = 0; p < ccen.size(); ++p) ccen[p] = cen[cl.perm[p]];
+        RTX_HIP(hipMemcpyAsync(c->d_ccen, ccen.data(), ccen.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cpre, cl.pre.data(), cl.pre.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cbnd, cl.bnd.data(), cl.bnd.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cperm, cl.perm.data(), cl.perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice,

@@ -35,20 +35,31 @@ struct KScene {
     float smag;
     float flat_cy;             // centre height shared by every sphere of blocks [flat_lo, flat_hi)
     uint32_t flat_lo, flat_hi;  // the scene's longest run of such flat blocks (empty: 0, 0)
-    // culled layout (lane-mode scan of scenes of kCullMinN..kCullMaxN spheres;
+    // culled layout (the lane-mode scan of scenes with n_pad > kScanPfMin;
     // NULL otherwise): the spheres in a spatial order, blocked like pre, with
     // each block's bounding sphere (rtx_prefilter.h cull_bound)
     //   cpre  float[n_cpad*4]  AoSoA-8 like pre (cx cy cz R), position order
     //   cbnd  float[ceil(n_cpad/64)*32]  AoSoA-8 groups of 8 block bounds (cx cy cz R_b)
+    //   cbnd2 float[ceil(n_cpad/512)*32] AoSoA-8 super-groups of 8 group bounds (each
+    //                          over the 64 spheres of a group of 8 blocks)
+    //   ccen  float4[n_cpad]   cen in position order (the resolve's sphere data)
     //   cperm uint32[n_cpad]   position -> scene index (a pad: a copy with R = -inf)
     // Blocks [cflat_lo, n_cpad/8) hold only spheres at height flat_cy.
     const float *cpre;
     const float *cbnd;
+    const float *cbnd2;
+    const float4 *ccen;
     const uint32_t *cperm;
     uint32_t n_cpad, cflat_lo;
 };
-constexpr uint32_t kCullMinN = 64;   // fewer spheres: the plain scan
-constexpr uint32_t kCullMaxN = 512;  // more: no room for the position map in the coop's LDS copy
+
+#ifndef RTX_CULL  // A/B build: 0 = no culled layout (the large-scene lane-mode scan visits every block)
+#define RTX_CULL 1
+#endif
+#ifndef RTX_SCAN_PF_MIN  // (A/B builds: 0 sends every scene to the kPF kernels)
+#define RTX_SCAN_PF_MIN 1024
+#endif
+constexpr uint32_t kScanPfMin = RTX_SCAN_PF_MIN;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
 
 constexpr uint32_t kPad = 8;  // spheres per AoSoA block
 

@@ -306,10 +306,6 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elem
 // Scalar loads return out of order, so the wait is lgkmcnt(0); it names the
 // loaded registers ("+s") so that nothing reads them before it. Every path
 // out of the loop body passes a wait, so no load is in flight at exit.
-#ifndef RTX_SCAN_PF_MIN  // (A/B builds: 0 sends every scene to the kPF kernels)
-#define RTX_SCAN_PF_MIN 1024
-#endif
-constexpr uint32_t kScanPfMin = RTX_SCAN_PF_MIN;  // scenes with n_pad above this take the kPF kernels (> 32 KiB of `pre`)
 #ifndef RTX_PACK  // kPF scans start where the workgroup's other waves are (hit_world_pre_ld)
 #define RTX_PACK 1
 #endif
@@ -651,7 +647,10 @@ __device__ __forceinline__ void resolve_one(float4 sc, int g, bool live, f3 o, f
 struct GiIdentity {
     __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return p; }
 };
-template <typename Ld, typename Gi = GiIdentity>
+// kPos: ld takes the list position (clamped to n - 1) instead of the scene
+// index (the culled layout keeps a copy of the spheres in position order, so
+// the data load and the index load are independent).
+template <typename Ld, typename Gi = GiIdentity, bool kPos = false>
 __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t *list, uint32_t m, f3 o, f3 d,
                                               float a, float inv_a, float t_min, float &best, int &idx,
                                               uint32_t cap = (uint32_t)kCand, Gi gi = Gi()) {
@@ -669,9 +668,12 @@ __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t 
     }
 #endif
     // next candidate: sphere index i (live = the lane has one), then advance
+    uint32_t pos = 0;  // (kPos) the position of the candidate next() returns
     auto next = [&](uint32_t &i, bool &live) {
         live = j < m;
-        i = gi((e & 0xffffffu) + (uint32_t)__builtin_ctz(live ? (e >> 24) : 1u));
+        pos = (e & 0xffffffu) + (uint32_t)__builtin_ctz(live ? (e >> 24) : 1u);
+        if constexpr (kPos) pos = min(pos, n - 1u);
+        i = gi(pos);
         e &= e - (1u << 24);  // drop that candidate from the mask
         const bool adv = live && (e >> 24) == 0u;
         j += adv ? 1u : 0u;
@@ -681,14 +683,14 @@ __device__ __forceinline__ bool resolve_pre_t(Ld ld, uint32_t n, const uint32_t 
     uint32_t i0;
     bool l0;
     next(i0, l0);
-    float4 v0 = ld(min(i0, n - 1u));
+    float4 v0 = kPos ? ld(pos) : ld(min(i0, n - 1u));
     uint64_t key = hit_key(best, idx);
     while (__ballot(l0) != 0ull) {
         RTX_DIAG_ADD(2, 1u);
         uint32_t i1;
         bool l1;
         next(i1, l1);
-        const float4 v1 = ld(min(i1, n - 1u));
+        const float4 v1 = kPos ? ld(pos) : ld(min(i1, n - 1u));
         resolve_one(v0, (int)i0, l0, o, d, a, inv_a, t_min, key, ok);
         i0 = i1;
         l0 = l1;
@@ -718,40 +720,41 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     uint32_t *my = list + threadIdx.x;
     const uint32_t nblk = S.n_cpad / 8u;
     const LineFlat K = line_test_flat(T, S.flat_cy);
-    const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
-    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
+    f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+    f2v ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
+    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
     const f2v th = {T.thr, T.thr};
     const float thr_b = T.thr * kCullThrScale;
-    // Q of 4 pairs of spheres (or bounds) of an AoSoA-8 block. The block's
-    // floats are read first, all of them, so that they arrive by a few wide
-    // scalar loads and one wait (read at their use, the compiler split them
-    // into pair loads with a wait in the middle).
-    auto quad = [&](auto flat, cfloat_p blk, f2v *q) {
-        float v[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i)
-            if (!decltype(flat)::value || i < 8 || i >= 16) v[i] = blk[i];
+    // Q of the 4 pairs of an AoSoA-8 block of spheres or bounds (blk(i): its i-th float)
+    auto quad = [&](auto flat, auto blk, f2v *q) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const f2v cx = {v[2 * p], v[2 * p + 1]};
-            const f2v cz = {v[16 + 2 * p], v[17 + 2 * p]};
-            const f2v R = {v[24 + 2 * p], v[25 + 2 * p]};
+            const f2v cx = {blk(2 * p), blk(2 * p + 1)};
+            const f2v cz = {blk(16 + 2 * p), blk(17 + 2 * p)};
+            const f2v R = {blk(24 + 2 * p), blk(25 + 2 * p)};
             f2v pu, pv;
             if constexpr (decltype(flat)::value) {
                 pu = fma2(cx, ux, fma2(cz, uz, ku));
                 pv = fma2(cz, vz, kv);
             } else {
-                const f2v cy = {v[8 + 2 * p], v[9 + 2 * p]};
+                const f2v cy = {blk(8 + 2 * p), blk(9 + 2 * p)};
                 pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
                 pv = fma2(cy, vy, fma2(cz, vz, nov));
             }
             q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
         }
     };
-    // one block of spheres: scan_range's finish (ballot, list entry)
+    // one block of spheres: scan_range's finish (ballot, list entry). Its
+    // floats are read first, all of them, so that they arrive by a few wide
+    // scalar loads and one wait.
     auto step = [&](auto flat, uint32_t bb) -> bool {
+        const cfloat_p blk = (cfloat_p)S.cpre + 32u * bb;
+        float v[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (!decltype(flat)::value || i < 8 || i >= 16) v[i] = blk[i];
         f2v q[4];
-        quad(flat, (cfloat_p)S.cpre + 32u * bb, q);
+        quad(flat, [&](int i) { return v[i]; }, q);
         const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
                                              q[2].y), q[3].x), q[3].y);
         RTX_DIAG_ADD(0, 1u);
@@ -767,56 +770,255 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
             const uint32_t mask = ~inv & 0xffu;
             my[cnt * kRB] = (8u * bb) | (mask << 24);
             cnt += mask != 0u ? 1u : 0u;
-            return __ballot(cnt == (uint32_t)kCand) != 0ull;
+            return __ballot(cnt == cand_of<true>()) != 0ull;
         }
         return false;
     };
     using Flat = std::integral_constant<bool, true>;
     using Full = std::integral_constant<bool, false>;
-    while (b < nblk) {
-        const uint32_t g = b >> 3;
+    // the wave-OR of the 8 bound tests of an AoSoA-8 group of bounds: bit j
+    // when some lane's line passes bound j (8 ballots)
+    auto bound_mask = [&](cfloat_p grp, bool flat) -> uint32_t {
+        float v[32];
         f2v q[4];
-        if (8u * g >= S.cflat_lo)
-            quad(Flat(), (cfloat_p)S.cbnd + 32u * g, q);
-        else
-            quad(Full(), (cfloat_p)S.cbnd + 32u * g, q);
+        if (flat) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+                if (i < 8 || i >= 16) v[i] = grp[i];
+            quad(Flat(), [&](int i) { return v[i]; }, q);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) v[i] = grp[i];
+            quad(Full(), [&](int i) { return v[i]; }, q);
+        }
         uint32_t m = 0;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             m |= (__ballot(!(q[p].x < thr_b)) != 0ull ? 1u : 0u) << (2 * p);
             m |= (__ballot(!(q[p].y < thr_b)) != 0ull ? 1u : 0u) << (2 * p + 1);
         }
-        const uint32_t left = nblk - 8u * g;
-        m &= (left >= 8u ? 0xffu : (1u << left) - 1u) & (0xffu << (b & 7u));
-        RTX_DIAG_ADD(6, (uint32_t)__popc(m));
-        while (m != 0u) {
-            const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            if (bb >= S.cflat_lo ? step(Flat(), bb) : step(Full(), bb)) return bb + 1u;
+        return m;
+    };
+    auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
+    // Two levels: a top bound covers the 64 spheres of a group of 8 blocks;
+    // the top bounds are tested 8 at a time (one "super-group": 64 blocks),
+    // then, for each passing group, its 8 block bounds, then the passing
+    // blocks' spheres. A resumed scan (b inside a super-group) masks off the
+    // groups and blocks before b.
+    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u;
+    for (uint32_t sg = b >> 6; sg < nsg; ++sg) {
+        uint32_t m2 = bound_mask((cfloat_p)S.cbnd2 + 32u * sg, 64u * sg >= S.cflat_lo);
+        m2 &= first_bits(ng - 8u * sg);
+        if (sg == (b >> 6)) m2 &= 0xffu << ((b >> 3) & 7u);
+        RTX_DIAG_ADD(6, (uint32_t)__popc(m2));
+        while (m2 != 0u) {
+            const uint32_t g = 8u * sg + (uint32_t)__builtin_ctz(m2);
+            m2 &= m2 - 1u;
+            uint32_t m = bound_mask((cfloat_p)S.cbnd + 32u * g, 8u * g >= S.cflat_lo);
+            m &= first_bits(nblk - 8u * g);
+            if (g == (b >> 3)) m &= 0xffu << (b & 7u);
+            while (m != 0u) {
+                const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                if (bb >= S.cflat_lo ? step(Flat(), bb) : step(Full(), bb)) return bb + 1u;
+            }
         }
-        b = 8u * g + 8u;
     }
+    return nblk;
+}
+
+// The culled scan with its loads staged through LDS (k_render's lane mode;
+// RTX_CULL_LDS). scan_culled's scalar loads wait one L2 round trip per
+// group test and per block (~1,100 per C5 wave-iteration). Here every level
+// arrives by LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes to LDS byte
+// 16 l of a 1-KiB slot, no registers) and is read back with broadcast
+// ds_read_b128: the top-level bounds stream through a ring of two slots (8
+// super-groups each, the next one in flight while this one is tested); for a
+// super-group whose test passes, ONE wave-wide DMA brings the 8 block bounds
+// of each passing group into slot G; for each passing group, one DMA brings
+// its passing blocks into slot B. Every lane of the wave runs this (the DMA
+// moves one piece per lane; `live` lanes have a ray, the others test against
+// thr = +inf and flag nothing). Waits are vmcnt (in order); every exit drains.
+#ifndef RTX_CULL_LDS
+#define RTX_CULL_LDS 0
+#endif
+constexpr uint32_t kCullWaveBytes = 4096;  // per wave: ring 2 KiB, G 1 KiB, B 1 KiB
+constexpr uint32_t kCullLdsBytes = (kRB / 64) * kCullWaveBytes;
+__device__ __forceinline__ uint32_t scan_culled_lds(const KScene &S, uint32_t b, const LineTest &T, uint32_t *list,
+                                                    uint32_t &cnt, float4 *wl) {
+    cnt = 0;
+    uint32_t *my = list + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nblk = S.n_cpad / 8u, ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u;
+    const LineFlat K = line_test_flat(T, S.flat_cy);
+    const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+    const f2v ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
+    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
+    const f2v th = {T.thr, T.thr};
+    const float thr_b = T.thr * kCullThrScale;
+    float4 *ring = wl, *G = wl + 128, *B = wl + 192;
+    const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(ring));
+    const uint32_t gbase = rbase + 2048u, bbase = rbase + 3072u;
+    const float4 *bnd2 = reinterpret_cast<const float4 *>(S.cbnd2);
+    const float4 *bnd = reinterpret_cast<const float4 *>(S.cbnd);
+    const float4 *pre = reinterpret_cast<const float4 *>(S.cpre);
+    using Flat = std::integral_constant<bool, true>;
+    using Full = std::integral_constant<bool, false>;
+    // Q of the 4 pairs of the AoSoA-8 block at LDS q (8 float4)
+    auto quad = [&](auto flat, const float4 *q, f2v *out) {
+        float4 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (!decltype(flat)::value || t < 2 || t >= 4) v[t] = q[t];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            auto f = [&](int i) {
+                const float4 w = v[i >> 2];
+                const int c = i & 3;
+                return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
+            };
+            const f2v cx = {f(2 * p), f(2 * p + 1)};
+            const f2v cz = {f(16 + 2 * p), f(17 + 2 * p)};
+            const f2v R = {f(24 + 2 * p), f(25 + 2 * p)};
+            f2v pu, pv;
+            if constexpr (decltype(flat)::value) {
+                pu = fma2(cx, ux, fma2(cz, uz, ku));
+                pv = fma2(cz, vz, kv);
+            } else {
+                const f2v cy = {f(8 + 2 * p), f(9 + 2 * p)};
+                pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+                pv = fma2(cy, vy, fma2(cz, vz, nov));
+            }
+            out[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+        }
+    };
+    auto bound_mask = [&](const float4 *q, bool flat) -> uint32_t {
+        f2v r[4];
+        if (flat)
+            quad(Flat(), q, r);
+        else
+            quad(Full(), q, r);
+        uint32_t m = 0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            m |= (__ballot(!(r[p].x < thr_b)) != 0ull ? 1u : 0u) << (2 * p);
+            m |= (__ballot(!(r[p].y < thr_b)) != 0ull ? 1u : 0u) << (2 * p + 1);
+        }
+        return m;
+    };
+    // the (lane >> 3)-th set bit of the uniform 8-bit mask m (8 if none)
+    auto nth_bit = [&](uint32_t m) -> uint32_t {
+        const uint32_t j = lane >> 3;
+        uint32_t pos = 8u, seen = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) {
+            const bool on = (m >> k) & 1u;
+            if (on && seen == j) pos = k;
+            seen += on ? 1u : 0u;
+        }
+        return pos;
+    };
+    auto drain = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+    // one block of spheres from slot B (its kb-th entry)
+    auto step = [&](auto flat, uint32_t kb, uint32_t bb) -> bool {
+        f2v q[4];
+        quad(flat, B + 8u * kb, q);
+        const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
+                                             q[2].y), q[3].x), q[3].y);
+        RTX_DIAG_ADD(0, 1u);
+        if (__ballot(!(mx < T.thr)) != 0ull) {
+            RTX_DIAG_ADD(1, 1u);
+            uint32_t inv = 0;
+#pragma unroll
+            for (int p = 3; p >= 0; --p) {
+                const f2v sq = q[p] - th;
+                inv = (inv << 1) | (__float_as_uint(sq.y) >> 31);
+                inv = (inv << 1) | (__float_as_uint(sq.x) >> 31);
+            }
+            const uint32_t mask = ~inv & 0xffu;
+            my[cnt * kRB] = (8u * bb) | (mask << 24);
+            cnt += mask != 0u ? 1u : 0u;
+            return __ballot(cnt == cand_of<true>()) != 0ull;
+        }
+        return false;
+    };
+    auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
+    auto issue_top = [&](uint32_t t, uint32_t slot) {
+        glds16(bnd2 + 8u * min(8u * t + (lane >> 3), nsg - 1u) + (lane & 7u), rbase + 1024u * slot);
+    };
+    const uint32_t sg0 = b >> 6, g0 = b >> 3;
+    uint32_t t = sg0 >> 3;
+    issue_top(t, 0u);
+    issue_top(t + 1u, 1u);
+    for (uint32_t j = 0;; ++j) {
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // tile t has landed (t + 1 may be in flight)
+        const float4 *tile = ring + 64u * (j & 1u);
+        for (uint32_t s8 = 0; s8 < 8u; ++s8) {
+            const uint32_t sg = 8u * t + s8;
+            if (sg >= nsg) break;
+            if (sg < sg0) continue;
+            uint32_t m2 = bound_mask(tile + 8u * s8, 64u * sg >= S.cflat_lo) & first_bits(ng - 8u * sg);
+            if (sg == sg0) m2 &= 0xffu << (g0 & 7u);
+            RTX_DIAG_ADD(6, (uint32_t)__popc(m2));
+            if (m2 == 0u) continue;
+            {  // the passing groups' block bounds into G (entry i: the i-th passing group)
+                const uint32_t k = nth_bit(m2);
+                if (k < 8u) glds16(bnd + 8u * (8u * sg + k) + (lane & 7u), gbase);
+                drain();
+            }
+            for (uint32_t i = 0; m2 != 0u; ++i) {
+                const uint32_t g = 8u * sg + (uint32_t)__builtin_ctz(m2);
+                m2 &= m2 - 1u;
+                uint32_t m = bound_mask(G + 8u * i, 8u * g >= S.cflat_lo) & first_bits(nblk - 8u * g);
+                if (g == g0) m &= 0xffu << (b & 7u);
+                if (m == 0u) continue;
+                {  // the passing blocks into B
+                    const uint32_t k = nth_bit(m);
+                    if (k < 8u) glds16(pre + 8u * (8u * g + k) + (lane & 7u), bbase);
+                    drain();
+                }
+                for (uint32_t kb = 0; m != 0u; ++kb) {
+                    const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    if (bb >= S.cflat_lo ? step(Flat(), kb, bb) : step(Full(), kb, bb)) {
+                        drain();  // the ring's next tiles
+                        return bb + 1u;
+                    }
+                }
+            }
+        }
+        if (8u * (t + 1u) >= nsg) break;
+        issue_top(t + 2u, j & 1u);  // into the slot just read (glds16 waits for its ds_reads first)
+        ++t;
+    }
+    drain();
     return nblk;
 }
 
 // hit_world over the culled layout: same (best, idx) as hit_world_pre (the
 // resolution rule is order-independent; the bounds never drop a reference
-// candidate). ld(i): (centre, radius) of scene sphere i; gi(p): the scene
-// index at layout position p < n_cpad.
-template <typename Ld, typename Gi>
-__device__ __forceinline__ int hit_world_culled(const KScene &S, Ld ld, Gi gi, f3 o, f3 d, float a, float inv_a,
-                                                float t_min, float &best, uint32_t *list) {
-    const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+// candidate). The resolve reads a candidate's (centre, radius) from ccen and
+// its scene index (the key's tie-break) from cperm, both by layout position.
+__device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
+                                                float &best, uint32_t *list, float4 *wl = nullptr, bool live = true) {
+    LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    if (!live) {  // a lane without a ray (the LDS-staged scan runs on every lane): nothing is flagged
+        T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
+        T.thr = __uint_as_float(0x7f800000u);
+    }
     const float best0 = best;
     int idx = -1;
     bool ok = true;
-    const uint32_t nblk = S.n_cpad / 8u, last = S.n_cpad - 1u;
-    auto gclamp = [gi, last](uint32_t p) { return gi(min(p, last)); };
+    const uint32_t nblk = S.n_cpad / 8u;
+    auto ld = [&S](uint32_t p) { return S.ccen[p]; };
+    auto gi = [&S](uint32_t p) { return S.cperm[p]; };
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = scan_culled(S, b, T, list, cnt);
-        ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, (uint32_t)kCand, gclamp) && ok;
+        b = wl ? scan_culled_lds(S, b, T, list, cnt, wl) : scan_culled(S, b, T, list, cnt);
+        ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
+                                                              idx, cand_of<true>(), gi) &&
+             ok;
     } while (b < nblk);
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
@@ -918,16 +1120,11 @@ __host__ __device__ constexpr uint32_t coop_lds_bytes(uint32_t n) {
     return coop_npad(n) * 4u * (uint32_t)sizeof(float) + n * (uint32_t)sizeof(float);
 }
 static_assert(coop_lds_bytes(kCoopLds) <= 12800, "LDS copy of the scene: 5 render blocks per CU");
-// ... plus the culled layout's position map (uint16, after the radii)
-__host__ __device__ constexpr uint32_t cull_lds_bytes(uint32_t n_cpad) { return (2u * n_cpad + 15u) / 16u * 16u; }
-static_assert(kCullMaxN <= kCoopLds && coop_lds_bytes(kCullMaxN) + cull_lds_bytes(kCullMaxN + 24u) <= 12800,
-              "the position map fits beside the LDS copy (3 sections padded: n_cpad <= n + 21)");
 
 struct SphLds {
     static constexpr bool kPadded = true;  // npairs is a multiple of 64: every group's steps stay inside
     const float *pr;   // [npairs][8]
     const float *rad;  // [n]
-    const uint16_t *perm;  // [n_cpad] the culled layout's position map (k_render with KScene::cpre), or unset
     uint32_t n, npairs;
     __device__ __forceinline__ void pair(uint32_t p, f2v &cx, f2v &cy, f2v &cz, f2v &R) const {
         const float4 *q = reinterpret_cast<const float4 *>(pr + 8u * p);
@@ -961,18 +1158,12 @@ struct SphGlobal {
 // Build the block's LDS copy (all threads of the block; the caller
 // synchronises): sphere i < npad at pair i/2, slot i%2 (copies of n - 1
 // beyond n), radii after the pairs.
-__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on, uint32_t nthreads = kRB,
-                                           bool with_perm = false) {
+__device__ __forceinline__ SphLds lds_copy(const KScene &S, float *base, bool on, uint32_t nthreads = kRB) {
     SphLds l;
     l.n = S.n;
     l.npairs = coop_npad(S.n) / 2u;
     l.pr = base;
     l.rad = base + 8u * l.npairs;
-    l.perm = reinterpret_cast<const uint16_t *>(base + 8u * l.npairs + S.n);
-    if (on && with_perm && S.cpre) {
-        uint16_t *pm = const_cast<uint16_t *>(l.perm);
-        for (uint32_t i = threadIdx.x; i < S.n_cpad; i += nthreads) pm[i] = (uint16_t)S.cperm[i];
-    }
     if (on) {
         float *pr = base, *rad = base + 8u * l.npairs;
         for (uint32_t i = threadIdx.x; i < 2u * l.npairs; i += nthreads) {
@@ -1139,6 +1330,131 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
         }
         __builtin_amdgcn_wave_barrier();
         RTX_CP(2)
+        if (mine) {
+            const uint32_t kb = keys[2 * rank], kc = keys[2 * rank + 1];
+            if (kb == 0xffffffffu) {
+                seq = true;
+            } else if (kb != 0u) {
+                const float c = __uint_as_float(kc);
+                if (c <= best) {  // accepted iff c <= t_max
+                    best = c;
+                    result = (int)(kb - 1u);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the next chunk reuses the LDS
+    }
+    return active ? result : -1;
+}
+
+// Group coop over the culled layout (large scenes: the frame tail, the
+// heavy tiers, promoted pixels). Same chunks, ray exchange, reduction and
+// `seq` rule as hit_world_groups; the scan is the culled one's hierarchy,
+// split over the group's g lanes: lane k tests the group bounds (the top
+// level, each over 64 spheres) k, k + g, ...; for a group its line passes,
+// the lane tests the group's 8 block bounds, then the spheres of the blocks
+// that pass, and resolves each flagged sphere on the spot (resolve_one:
+// ccen and cperm by layout position). Lanes diverge inside a passing group;
+// a ray's line passes ~2 % of the C5 scene's groups, so a 64-lane ray
+// visits about one group per lane instead of scanning 1,563 spheres per
+// lane. Bounds and spheres use the 7-op test (the margins cover it on
+// flat blocks too, rtx_prefilter.h).
+__device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t act, bool active, f3 o, f3 d,
+                                                       float a, float inv_a, float t_min, float *ws, float &best,
+                                                       bool &seq) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m_all = (uint32_t)__popcll(act);
+    const uint32_t rank_all =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    uint32_t *keys = reinterpret_cast<uint32_t *>(ws + 8 * kGfRays);
+    const float inf = __uint_as_float(0x7f800000u);
+    const uint32_t nblk = S.n_cpad / 8u, ngrp = (nblk + 7u) / 8u;
+    int result = -1;
+    seq = false;
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < m_all; c0 += kGfRays) {
+        const uint32_t m = min(m_all - c0, kGfRays);
+        const bool mine = active && rank_all >= c0 && rank_all < c0 + m;
+        const uint32_t rank = rank_all - c0;
+        if (mine) {
+            float *w = ws + 8 * rank;
+            w[0] = o.x;
+            w[1] = o.y;
+            w[2] = o.z;
+            w[3] = d.x;
+            w[4] = d.y;
+            w[5] = d.z;
+            w[6] = a;
+            w[7] = inv_a;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t lg = m <= 1u ? 6u : 6u - (32u - (uint32_t)__builtin_clz(m - 1u));  // log2(g)
+        const uint32_t g = 1u << lg;
+        const uint32_t r = lane >> lg, k = lane & (g - 1u);
+        const bool valid = r < m;
+        const float *w = ws + 8 * (valid ? r : 0u);
+        const f3 ro = mk3(w[0], w[1], w[2]), rd = mk3(w[3], w[4], w[5]);
+        const float ra = w[6], ria = w[7];
+        const LineTest T = line_test_setup(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ra, S.smag);
+        const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
+        const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
+        const float thr_b = T.thr * kCullThrScale;
+        // bit j: entry j of an AoSoA-8 block (bounds or spheres) passes Q >= thr
+        auto block_mask = [&](const float *blk, float thr) -> uint32_t {
+            const float4 *b4 = reinterpret_cast<const float4 *>(blk);
+            float4 v[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = b4[t];
+            uint32_t msk = 0;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const float4 X = v[p >> 1], Y = v[2 + (p >> 1)], Z = v[4 + (p >> 1)], Rr = v[6 + (p >> 1)];
+                const bool hi = p & 1;
+                const f2v cx = {hi ? X.z : X.x, hi ? X.w : X.y}, cy = {hi ? Y.z : Y.x, hi ? Y.w : Y.y};
+                const f2v cz = {hi ? Z.z : Z.x, hi ? Z.w : Z.y}, R = {hi ? Rr.z : Rr.x, hi ? Rr.w : Rr.y};
+                const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
+                const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
+                const f2v q = fma2(-pv, pv, fma2(-pu, pu, R));
+                msk |= (!(q.x < thr) ? 1u : 0u) << (2 * p);
+                msk |= (!(q.y < thr) ? 1u : 0u) << (2 * p + 1);
+            }
+            return msk;
+        };
+        uint64_t key = hit_key(inf, -1);
+        bool ok = true;
+        const uint32_t nsteps = valid ? (ngrp + g - 1u) >> lg : 0u;
+#pragma unroll 1
+        for (uint32_t st = 0; st < nsteps; ++st) {
+            const uint32_t gi = (st << lg) + k;
+            if (gi >= ngrp) break;
+            const float *gb = S.cbnd2 + 32u * (gi >> 3) + (gi & 7u);
+            if (line_test_q(T, gb[0], gb[8], gb[16], gb[24]) < thr_b) continue;
+            const uint32_t left = nblk - 8u * gi;
+            uint32_t mb = block_mask(S.cbnd + 32u * gi, thr_b) & (left >= 8u ? 0xffu : (1u << left) - 1u);
+#pragma unroll 1
+            while (mb != 0u) {
+                const uint32_t bb = 8u * gi + (uint32_t)__builtin_ctz(mb);
+                mb &= mb - 1u;
+                uint32_t ms = block_mask(S.cpre + 32u * bb, T.thr);
+#pragma unroll 1
+                while (ms != 0u) {
+                    const uint32_t pos = 8u * bb + (uint32_t)__builtin_ctz(ms);
+                    ms &= ms - 1u;
+                    resolve_one(S.ccen[pos], (int)S.cperm[pos], true, ro, rd, ra, ria, t_min, key, ok);
+                }
+            }
+        }
+        // the group's (min c, then the largest index among equal c)
+        const uint32_t cb0 = (uint32_t)(key >> 32);
+        const uint32_t cb = group_reduce_u32<false>(cb0, lg);
+        const uint32_t ib = group_reduce_u32<true>(cb0 == cb ? ~(uint32_t)key : 0u, lg);  // index + 1, 0: none
+        const uint64_t badm = __ballot(!ok);
+        if (valid && k == 0u) {
+            const uint64_t gm = (g == 64u ? ~0ull : ((1ull << g) - 1ull)) << (r * g);
+            keys[2 * r] = (badm & gm) != 0ull ? 0xffffffffu : ib;  // ~0: a non-finite root in the group
+            keys[2 * r + 1] = cb;
+        }
+        __builtin_amdgcn_wave_barrier();
         if (mine) {
             const uint32_t kb = keys[2 * rank], kc = keys[2 * rank + 1];
             if (kb == 0xffffffffu) {
@@ -1976,7 +2292,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
     (void)coop_ws;
     // the coop's sphere data: a block-wide LDS copy for small scenes (SphLds)
     const bool coop_lds = P.scene.n <= kCoopLds;
-    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds, kRB, !kPF);
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds);
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
@@ -2068,10 +2384,13 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
             bool promoted = false;
-            int my_hit = coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
-                                                     coop_ws, my_best, my_seq, cp, ctqp)
-                                  : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
-                                                     coop_ws, my_best, my_seq, cp, ctqp);
+            int my_hit = (kPF && RTX_CULL)
+                             ? hit_world_groups_culled(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws,
+                                                       my_best, my_seq)
+                         : coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
+                                                       coop_ws, my_best, my_seq, cp, ctqp)
+                                    : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
+                                                       coop_ws, my_best, my_seq, cp, ctqp);
             if (L.active) {
                 if (my_seq) {  // (rare: the plain scan, so the kPF ping-pong's SGPRs stay out of this kernel)
                     my_best = __uint_as_float(0x7f800000u);
@@ -2101,7 +2420,20 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         }
         bool promoted = false;
         D.rays(P, L.o, L.d, L.active, L.slot);
-        if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
+        if (kPF && RTX_CULL && RTX_CULL_LDS) {  // large scenes: the culled scan, LDS-staged (every lane runs it)
+            float best = __uint_as_float(0x7f800000u);
+            float4 *wl = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes + 16) + (threadIdx.x / 64u) * 256u;
+            const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, wl, L.active);
+            D.section(1);
+            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
+        } else if (kPF && RTX_CULL) {  // large scenes: the culled scan (block bounds first, scan_culled)
+            if (L.active) {
+                float best = __uint_as_float(0x7f800000u);
+                const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+                D.section(1);
+                promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
+            }
+        } else if ((RTX_PF_LDS || RTX_PF_RING) && kPF) {  // every lane of the wave fills the scan's LDS tile
             float best = __uint_as_float(0x7f800000u);
             auto ldc = [&P](uint32_t i) { return P.scene.cen[i]; };
             const int hit = hit_world_pre_ld<kPF, decltype(ldc), true>(P.scene, ldc, L.o, L.d, L.a, L.inv_a, kTMin,
@@ -2111,15 +2443,11 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         } else if (L.active) {
             float best = __uint_as_float(0x7f800000u);
             // scenes that fit the coop's LDS copy resolve their candidates
-            // from it (the same centre and radius floats as cen) instead of
-            // HBM/L2; with a culled layout they scan it (scan_culled)
-            auto lds_sph = [sl](uint32_t i) { return sl.sphere(i); };
-            const int hit = (!kPF && coop_lds && P.scene.cpre)
-                                ? hit_world_culled(P.scene, lds_sph, [sl](uint32_t p) { return (uint32_t)sl.perm[p]; },
-                                                   L.o, L.d, L.a, L.inv_a, kTMin, best, list)
-                            : (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
-                                ? hit_world_pre_ld<kPF>(P.scene, lds_sph, L.o, L.d, L.a, L.inv_a, kTMin, best, list,
-                                                        nullptr, 0, RTX_SCAN_LDS ? sl.pr : nullptr)
+            // from it (the same centre and radius floats as cen) instead of HBM/L2
+            const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
+                                ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
+                                                        L.a, L.inv_a, kTMin, best, list, nullptr, 0,
+                                                        RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
             promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
@@ -2671,18 +2999,21 @@ __global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
         if (exhausted && __popcll(act) <= kCoopMax) {  // the wave's last few samples: group coop
             __builtin_amdgcn_s_setprio(kTailPrio);
             bool seq = false;
-            hit = sph_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
-                                             seq)
-                          : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
-                                             seq);
+            hit = (kPF && RTX_CULL)
+                      ? hit_world_groups_culled(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best, seq)
+                  : sph_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
+                                               seq)
+                            : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
+                                               seq);
             if (L.active && seq) {  // a non-finite root in the group: the exact path
                 best = __uint_as_float(0x7f800000u);
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
-            hit = sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
-                                                  L.inv_a, kTMin, best, list)
-                          : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+            hit = (kPF && RTX_CULL) ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+                  : sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
+                                                    L.inv_a, kTMin, best, list)
+                            : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
         }
         if (L.active) {
             L.segs++;
@@ -2776,8 +3107,7 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     float best = t_max;
     const int idx =
         min((start == kDebugCulled && S.cpre)
-                ? hit_world_culled(S, [&S](uint32_t j) { return S.cen[min(j, S.n - 1u)]; },
-                                   [&S](uint32_t p) { return S.cperm[p]; }, o, d, a, inv_a, t_min, best, list)
+                ? hit_world_culled(S, o, d, a, inv_a, t_min, best, list)
             : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
                                    : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
@@ -2813,7 +3143,7 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
 __global__ void RTX_RENDER_BOUNDS k_debug_scan_rate(const KParams P, uint32_t reps, unsigned long long *sink) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
-    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kListBytes + kCoopBytes), true, kRB, true);
+    const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kListBytes + kCoopBytes), true);
     __syncthreads();
     const uint32_t npix = P.rows_local * P.width;
     const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
@@ -2828,13 +3158,8 @@ __global__ void RTX_RENDER_BOUNDS k_debug_scan_rate(const KParams P, uint32_t re
     uint32_t acc = 0;
     for (uint32_t r = 0; r < reps; ++r) {
         float best = __uint_as_float(0x7f800000u);
-        const int hit = P.scene.cpre
-                            ? hit_world_culled(P.scene, [sl](uint32_t i) { return sl.sphere(i); },
-                                               [sl](uint32_t p) { return (uint32_t)sl.perm[p]; }, o, d, a, inv_a,
-                                               kTMin, best, list)
-                            : hit_world_pre_ld<false>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, o, d, a,
-                                                      inv_a, kTMin, best, list, nullptr, 0,
-                                                      RTX_SCAN_LDS ? sl.pr : nullptr);
+        const int hit = hit_world_pre_ld<false>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, o, d, a, inv_a,
+                                                kTMin, best, list, nullptr, 0, RTX_SCAN_LDS ? sl.pr : nullptr);
         acc += (uint32_t)hit ^ __float_as_uint(best);
     }
 #pragma unroll
@@ -2935,8 +3260,9 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() + 16 + kPfLdsBytes : kListBytes) + kCoopBytes +  // kPF: the pack word
-           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) + (s.cpre ? cull_lds_bytes(s.n_cpad) : 0u) : 0);
+    return (use_pf(s) ? list_bytes<true>() + 16 + (RTX_CULL ? (RTX_CULL_LDS ? kCullLdsBytes : 0u) : kPfLdsBytes)
+                      : kListBytes) + kCoopBytes +  // kPF: the pack word, then the culled scan's slots (or the tile)
+           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
@@ -3185,8 +3511,7 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
 hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
                                   hipStream_t stream) {
     if (p.scene.n > kCoopLds || use_pf(p.scene) || (uint64_t)p.rows_local * p.width == 0) return hipErrorInvalidValue;
-    const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n) +
-                       (p.scene.cpre ? cull_lds_bytes(p.scene.n_cpad) : 0u);
+    const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n);
     const uint32_t blocks = resident_blocks((const void *)k_debug_scan_rate, lds);
     *waves = blocks * (kRB / 64);
     hipLaunchKernelGGL(k_debug_scan_rate, dim3(blocks), dim3(kRB), lds, stream, p, reps, sink);

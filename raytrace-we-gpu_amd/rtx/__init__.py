@@ -422,7 +422,7 @@ class Context:
                         t_max: float = float("inf"), start_block: Optional[int] = None) -> np.ndarray:
         """hit_world on the GPU (rtx_debug_hit_world); start_block: the scan
         starts at that 8-sphere block and wraps round (rtx_debug_hit_world_from);
-        DEBUG_CULLED: the culled scan (worlds of 64..512 spheres)."""
+        DEBUG_CULLED: the culled scan (worlds of more than 1,024 spheres)."""
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
         out = np.zeros((rays.shape[0], 10), np.float32)
         if start_block is None:

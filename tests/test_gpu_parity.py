@@ -147,7 +147,8 @@ def test_hit_world_wrapped_scan_starts(gpu_ctx, oracle, rtx, which):
     the resolution rule must give the in-order answer from every start —
     rtx_debug_hit_world_from at start blocks 0, 1, mid, nblk - 1 and beyond,
     on the 100k-sphere golden case and on a scene of duplicated spheres
-    whose ties straddle the wrap point."""
+    whose ties straddle the wrap point; and the culled scan (spatial order)
+    on both."""
     if which == "c5_100k":
         c = load_case("hit_c5_100k.npz", 0, lambda ext, cap: rtx.random_world(ext, capacity=cap).spheres)
         sph, rays, t_min = c["spheres"], c["rays"].astype(np.float32), c["t_min"]
@@ -164,7 +165,7 @@ def test_hit_world_wrapped_scan_starts(gpu_ctx, oracle, rtx, which):
     gpu_ctx.upload_world(world)
     want = oracle.hit_world_f32(world, rays, t_min)
     nblk = (n + 7) // 8
-    for start in (0, 1, nblk // 2, nblk - 1, nblk + 3):
+    for start in (0, 1, nblk // 2, nblk - 1, nblk + 3, rtx.DEBUG_CULLED):
         got = gpu_ctx.debug_hit_world(rays, t_min=t_min, start_block=start)
         assert_bits_equal(got, want, f"{which}: scan from block {start} of {nblk}")
     if which == "ties":
@@ -179,10 +180,11 @@ def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx, scan):
     axis (the prefilter basis's degenerate direction), tiny and huge
     direction lengths (some outside the prefilter's safe range) and origins
     far down the line: the kernel's prefiltered scan (rtx_prefilter.h) must
-    return the reference scan's records bit for bit — the plain scan and the
-    culled one (block bounds first, spatial order, position map)."""
+    return the reference scan's records bit for bit — the plain scan (the
+    486-sphere scene) and the culled one (block bounds first, spatial order,
+    position map; a 2,504-sphere random scene)."""
     rng = np.random.default_rng(11)
-    world = rtx.random_world(11, depth=1, spp=1)
+    world = rtx.random_world(11 if scan == "plain" else 25, depth=1, spp=1)
     rays = grazing_rays(world.spheres, 30000, rng, xaxis_frac=0.05)
     gpu_ctx.upload_world(world)
     got = gpu_ctx.debug_hit_world(rays, start_block=rtx.DEBUG_CULLED if scan == "culled" else None)
@@ -191,21 +193,22 @@ def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx, scan):
     assert (want[:, 0] == 1).mean() > 0.3
 
 
-@pytest.mark.parametrize("n", [64, 65, 130, 333, 486, 512])
+@pytest.mark.parametrize("n", [1025, 1100, 1500, 4100, 12000])
 def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
-    """The culled scan (DESIGN.md §3 "culled scan") on scenes across its size
+    """The culled scan (DESIGN.md §3e "culled scan") on scenes across its size
     range: random spheres at mixed heights, a flat run at one height (the 5-op
     bound test), a few large spheres (their own section) and duplicated
     spheres whose ties must still go to the later index though the layout
-    reorders them; rays aimed at spheres, random ones and grazing ones, with
-    t_min's near the tie roots."""
+    reorders them; rays aimed at spheres, random ones and grazing ones, at
+    two t_min's."""
     rng = np.random.default_rng(n)
     k = n // 3
-    flat = np.concatenate([rng.uniform(-11, 11, (k, 1)), np.full((k, 1), 0.2), rng.uniform(-11, 11, (k, 1)),
+    ext = 11.0 * np.sqrt(n / 486.0)  # the RTIOW density
+    flat = np.concatenate([rng.uniform(-ext, ext, (k, 1)), np.full((k, 1), 0.2), rng.uniform(-ext, ext, (k, 1)),
                            np.full((k, 1), 0.2)], 1)
     big = np.array([[0, -1000, 0, 1000], [0, 1, 0, 1.0], [-4, 1, 0, 1.0], [4, 1, 0, 1.0]])
     m = n - k - len(big) - 8
-    other = np.concatenate([rng.uniform(-11, 11, (m, 1)), rng.uniform(0, 3, (m, 1)), rng.uniform(-11, 11, (m, 1)),
+    other = np.concatenate([rng.uniform(-ext, ext, (m, 1)), rng.uniform(0, 3, (m, 1)), rng.uniform(-ext, ext, (m, 1)),
                             rng.uniform(0.1, 0.5, (m, 1))], 1)
     sph = np.concatenate([big[:1], other, flat, big[1:]]).astype(np.float32)
     dup_src = rng.choice(len(sph) - 1, 8, replace=False) + 1
@@ -213,10 +216,10 @@ def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
     assert len(sph) == n
     world = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
     gpu_ctx.upload_world(world)
-    o = rng.uniform(-14, 14, (6000, 3)) + np.array([0, 8, 0])
+    o = rng.uniform(-ext - 3, ext + 3, (6000, 3)) * np.array([1, 0.3, 1]) + np.array([0, 8, 0])
     d = (sph[rng.integers(1, n, 6000), :3] - o) + rng.normal(scale=0.15, size=(6000, 3))
     rays = np.concatenate([np.concatenate([o, d], 1), grazing_rays(sph, 6000, rng, xaxis_frac=0.05),
-                           np.concatenate([rng.uniform(-12, 12, (3000, 3)), rng.normal(size=(3000, 3))], 1)])
+                           np.concatenate([rng.uniform(-ext, ext, (3000, 3)), rng.normal(size=(3000, 3))], 1)])
     rays = rays.astype(np.float32)
     for t_min in (0.001, 0.5):
         want = oracle.hit_world_f32(world, rays, t_min)
