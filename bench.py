@@ -307,7 +307,8 @@ def roofline_of(executed, launch_ms, tests_per_launch):
         r["frac_kind"] += " (needs the N=1 PMC passes: not run here)"
     r.update(effective_tflops=round(eff, 3),
              effective_note="20 FLOP x (segments x spheres) per launch / launch time: the reference algorithm's "
-                            "work rate, not a fraction of any roof")
+                            "work rate (every sphere tested per segment), not a fraction of any roof; large "
+                            "scenes skip most spheres (culled scan), so there it exceeds the peak")
     return r
 
 
@@ -439,10 +440,11 @@ def launch_desc(n_spheres, spp, nparts, rng):
     if spp < 8 and rng == "chain":
         return "rtx_render_rows launch = k_render<false> (exact grid, one lane per pixel)"
     large = ((n_spheres + 7) // 8) * 8 > 1024  # kScanPfMin: the kPF kernels
-    scan = ("lane-mode scan streamed through a per-wave LDS tile, candidate lists of 24"
+    scan = ("culled scan over a spatially ordered copy of the scene (group bounds, block bounds, spheres;"
+            " the coop tiers split the same hierarchy over a ray's lanes), candidate lists of 24"
             if large else "scalar-loaded scan, resolve from the block's LDS copy of the scene")
     if rng == "per-sample":
-        return f"k_render_ps (one lane per pixel-sample, in-order fold per pixel; {scan.split(',')[0]})"
+        return f"k_render_ps (one lane per pixel-sample, in-order fold per pixel; {scan.split(' (')[0]})"
     whole = nparts == 1
     if large:
         pre = ("k_render<true,true,kPF> 1-spp cost pre-pass on persistent lanes (sample 0, resumed from"

@@ -198,6 +198,10 @@ constexpr uint32_t kRB = 256;           // threads per render workgroup
 #define RTX_WAVES_PER_SIMD_PF 4
 #endif
 #define RTX_RENDER_BOUNDS_T(kPF) __launch_bounds__(kRB, (kPF) ? RTX_WAVES_PER_SIMD_PF : RTX_WAVES_PER_SIMD)
+#ifndef RTX_PS_WAVES_PF  // the per-sample kernel's large-scene instance (A/B: 4 = 128 VGPRs)
+#define RTX_PS_WAVES_PF RTX_WAVES_PER_SIMD
+#endif
+#define RTX_PS_BOUNDS_T(kPF) __launch_bounds__(kRB, (kPF) ? RTX_PS_WAVES_PF : RTX_WAVES_PER_SIMD)
 
 // Candidate list: per lane kCand slots in LDS, slot-major
 // (slot j of lane t at [j * kRB + t]: conflict-free), plus one dump slot
@@ -827,185 +831,13 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     return nblk;
 }
 
-// The culled scan with its loads staged through LDS (k_render's lane mode;
-// RTX_CULL_LDS). scan_culled's scalar loads wait one L2 round trip per
-// group test and per block (~1,100 per C5 wave-iteration). Here every level
-// arrives by LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes to LDS byte
-// 16 l of a 1-KiB slot, no registers) and is read back with broadcast
-// ds_read_b128: the top-level bounds stream through a ring of two slots (8
-// super-groups each, the next one in flight while this one is tested); for a
-// super-group whose test passes, ONE wave-wide DMA brings the 8 block bounds
-// of each passing group into slot G; for each passing group, one DMA brings
-// its passing blocks into slot B. Every lane of the wave runs this (the DMA
-// moves one piece per lane; `live` lanes have a ray, the others test against
-// thr = +inf and flag nothing). Waits are vmcnt (in order); every exit drains.
-#ifndef RTX_CULL_LDS
-#define RTX_CULL_LDS 0
-#endif
-constexpr uint32_t kCullWaveBytes = 4096;  // per wave: ring 2 KiB, G 1 KiB, B 1 KiB
-constexpr uint32_t kCullLdsBytes = (kRB / 64) * kCullWaveBytes;
-__device__ __forceinline__ uint32_t scan_culled_lds(const KScene &S, uint32_t b, const LineTest &T, uint32_t *list,
-                                                    uint32_t &cnt, float4 *wl) {
-    cnt = 0;
-    uint32_t *my = list + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nblk = S.n_cpad / 8u, ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u;
-    const LineFlat K = line_test_flat(T, S.flat_cy);
-    const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
-    const f2v ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
-    const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
-    const f2v th = {T.thr, T.thr};
-    const float thr_b = T.thr * kCullThrScale;
-    float4 *ring = wl, *G = wl + 128, *B = wl + 192;
-    const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(ring));
-    const uint32_t gbase = rbase + 2048u, bbase = rbase + 3072u;
-    const float4 *bnd2 = reinterpret_cast<const float4 *>(S.cbnd2);
-    const float4 *bnd = reinterpret_cast<const float4 *>(S.cbnd);
-    const float4 *pre = reinterpret_cast<const float4 *>(S.cpre);
-    using Flat = std::integral_constant<bool, true>;
-    using Full = std::integral_constant<bool, false>;
-    // Q of the 4 pairs of the AoSoA-8 block at LDS q (8 float4)
-    auto quad = [&](auto flat, const float4 *q, f2v *out) {
-        float4 v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-            if (!decltype(flat)::value || t < 2 || t >= 4) v[t] = q[t];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            auto f = [&](int i) {
-                const float4 w = v[i >> 2];
-                const int c = i & 3;
-                return c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
-            };
-            const f2v cx = {f(2 * p), f(2 * p + 1)};
-            const f2v cz = {f(16 + 2 * p), f(17 + 2 * p)};
-            const f2v R = {f(24 + 2 * p), f(25 + 2 * p)};
-            f2v pu, pv;
-            if constexpr (decltype(flat)::value) {
-                pu = fma2(cx, ux, fma2(cz, uz, ku));
-                pv = fma2(cz, vz, kv);
-            } else {
-                const f2v cy = {f(8 + 2 * p), f(9 + 2 * p)};
-                pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
-                pv = fma2(cy, vy, fma2(cz, vz, nov));
-            }
-            out[p] = fma2(-pv, pv, fma2(-pu, pu, R));
-        }
-    };
-    auto bound_mask = [&](const float4 *q, bool flat) -> uint32_t {
-        f2v r[4];
-        if (flat)
-            quad(Flat(), q, r);
-        else
-            quad(Full(), q, r);
-        uint32_t m = 0;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            m |= (__ballot(!(r[p].x < thr_b)) != 0ull ? 1u : 0u) << (2 * p);
-            m |= (__ballot(!(r[p].y < thr_b)) != 0ull ? 1u : 0u) << (2 * p + 1);
-        }
-        return m;
-    };
-    // the (lane >> 3)-th set bit of the uniform 8-bit mask m (8 if none)
-    auto nth_bit = [&](uint32_t m) -> uint32_t {
-        const uint32_t j = lane >> 3;
-        uint32_t pos = 8u, seen = 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) {
-            const bool on = (m >> k) & 1u;
-            if (on && seen == j) pos = k;
-            seen += on ? 1u : 0u;
-        }
-        return pos;
-    };
-    auto drain = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-    // one block of spheres from slot B (its kb-th entry)
-    auto step = [&](auto flat, uint32_t kb, uint32_t bb) -> bool {
-        f2v q[4];
-        quad(flat, B + 8u * kb, q);
-        const float mx = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(q[0].x, q[0].y), q[1].x), q[1].y), q[2].x),
-                                             q[2].y), q[3].x), q[3].y);
-        RTX_DIAG_ADD(0, 1u);
-        if (__ballot(!(mx < T.thr)) != 0ull) {
-            RTX_DIAG_ADD(1, 1u);
-            uint32_t inv = 0;
-#pragma unroll
-            for (int p = 3; p >= 0; --p) {
-                const f2v sq = q[p] - th;
-                inv = (inv << 1) | (__float_as_uint(sq.y) >> 31);
-                inv = (inv << 1) | (__float_as_uint(sq.x) >> 31);
-            }
-            const uint32_t mask = ~inv & 0xffu;
-            my[cnt * kRB] = (8u * bb) | (mask << 24);
-            cnt += mask != 0u ? 1u : 0u;
-            return __ballot(cnt == cand_of<true>()) != 0ull;
-        }
-        return false;
-    };
-    auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
-    auto issue_top = [&](uint32_t t, uint32_t slot) {
-        glds16(bnd2 + 8u * min(8u * t + (lane >> 3), nsg - 1u) + (lane & 7u), rbase + 1024u * slot);
-    };
-    const uint32_t sg0 = b >> 6, g0 = b >> 3;
-    uint32_t t = sg0 >> 3;
-    issue_top(t, 0u);
-    issue_top(t + 1u, 1u);
-    for (uint32_t j = 0;; ++j) {
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // tile t has landed (t + 1 may be in flight)
-        const float4 *tile = ring + 64u * (j & 1u);
-        for (uint32_t s8 = 0; s8 < 8u; ++s8) {
-            const uint32_t sg = 8u * t + s8;
-            if (sg >= nsg) break;
-            if (sg < sg0) continue;
-            uint32_t m2 = bound_mask(tile + 8u * s8, 64u * sg >= S.cflat_lo) & first_bits(ng - 8u * sg);
-            if (sg == sg0) m2 &= 0xffu << (g0 & 7u);
-            RTX_DIAG_ADD(6, (uint32_t)__popc(m2));
-            if (m2 == 0u) continue;
-            {  // the passing groups' block bounds into G (entry i: the i-th passing group)
-                const uint32_t k = nth_bit(m2);
-                if (k < 8u) glds16(bnd + 8u * (8u * sg + k) + (lane & 7u), gbase);
-                drain();
-            }
-            for (uint32_t i = 0; m2 != 0u; ++i) {
-                const uint32_t g = 8u * sg + (uint32_t)__builtin_ctz(m2);
-                m2 &= m2 - 1u;
-                uint32_t m = bound_mask(G + 8u * i, 8u * g >= S.cflat_lo) & first_bits(nblk - 8u * g);
-                if (g == g0) m &= 0xffu << (b & 7u);
-                if (m == 0u) continue;
-                {  // the passing blocks into B
-                    const uint32_t k = nth_bit(m);
-                    if (k < 8u) glds16(pre + 8u * (8u * g + k) + (lane & 7u), bbase);
-                    drain();
-                }
-                for (uint32_t kb = 0; m != 0u; ++kb) {
-                    const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    if (bb >= S.cflat_lo ? step(Flat(), kb, bb) : step(Full(), kb, bb)) {
-                        drain();  // the ring's next tiles
-                        return bb + 1u;
-                    }
-                }
-            }
-        }
-        if (8u * (t + 1u) >= nsg) break;
-        issue_top(t + 2u, j & 1u);  // into the slot just read (glds16 waits for its ds_reads first)
-        ++t;
-    }
-    drain();
-    return nblk;
-}
-
 // hit_world over the culled layout: same (best, idx) as hit_world_pre (the
 // resolution rule is order-independent; the bounds never drop a reference
 // candidate). The resolve reads a candidate's (centre, radius) from ccen and
 // its scene index (the key's tie-break) from cperm, both by layout position.
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
-                                                float &best, uint32_t *list, float4 *wl = nullptr, bool live = true) {
-    LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
-    if (!live) {  // a lane without a ray (the LDS-staged scan runs on every lane): nothing is flagged
-        T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
-        T.thr = __uint_as_float(0x7f800000u);
-    }
+                                                float &best, uint32_t *list) {
+    const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const float best0 = best;
     int idx = -1;
     bool ok = true;
@@ -1015,7 +847,7 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = wl ? scan_culled_lds(S, b, T, list, cnt, wl) : scan_culled(S, b, T, list, cnt);
+        b = scan_culled(S, b, T, list, cnt);
         ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
                                                               idx, cand_of<true>(), gi) &&
              ok;
@@ -2420,13 +2252,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         }
         bool promoted = false;
         D.rays(P, L.o, L.d, L.active, L.slot);
-        if (kPF && RTX_CULL && RTX_CULL_LDS) {  // large scenes: the culled scan, LDS-staged (every lane runs it)
-            float best = __uint_as_float(0x7f800000u);
-            float4 *wl = reinterpret_cast<float4 *>(s_mem + kLB + kCoopBytes + 16) + (threadIdx.x / 64u) * 256u;
-            const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, wl, L.active);
-            D.section(1);
-            if (L.active) promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
-        } else if (kPF && RTX_CULL) {  // large scenes: the culled scan (block bounds first, scan_culled)
+        if (kPF && RTX_CULL) {  // large scenes: the culled scan (block bounds first, scan_culled)
             if (L.active) {
                 float best = __uint_as_float(0x7f800000u);
                 const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -2928,7 +2754,7 @@ __device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t
 }
 
 template <bool kPF>
-__global__ void RTX_RENDER_BOUNDS k_render_ps(const KParams P) {
+__global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][batch slots, kPsStateBytes]
     //              [LDS copy of the spheres (n <= kCoopLds)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -3260,8 +3086,7 @@ static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, c
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() + 16 + (RTX_CULL ? (RTX_CULL_LDS ? kCullLdsBytes : 0u) : kPfLdsBytes)
-                      : kListBytes) + kCoopBytes +  // kPF: the pack word, then the culled scan's slots (or the tile)
+    return (use_pf(s) ? list_bytes<true>() + 16 + (RTX_CULL ? 0u : kPfLdsBytes) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
            (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
