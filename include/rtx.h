@@ -40,8 +40,9 @@ extern "C" {
 
 #define RTX_VERSION 142 /* 1.4.2 */
 /* ABI notes.
- *  1.4.2: rtx_debug_hit_world_from's start_block RTX_DEBUG_CULLED (the
- *         culled scan; no layout change).
+ *  1.4.2: rtx_debug_hit_world_from's start_block RTX_DEBUG_CULLED and
+ *         RTX_DEBUG_CULLED_COOP(q) (the culled scan, lane mode and group
+ *         coop; no layout change).
  *  1.4.1: rtx_debug_scan_rate (a diagnostic; no layout change).
  *  1.4.0: rtx_schedule.prio_bar1..3 (after prepass_cap_split, before
  *         `reserved`): dynamic lane-mode wave priority; the struct grew by
@@ -405,6 +406,10 @@ RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
  * "culled scan"); smaller worlds scan from block
  * RTX_DEBUG_CULLED % ceil(count / 8) as above. */
 #define RTX_DEBUG_CULLED 0xFFFFFFFFu
+/* start_block = RTX_DEBUG_CULLED_COOP(q), q in 1..64, for the same worlds:
+ * the culled scan split over a wave's lanes as the render's frame tail and
+ * heavy tiers run it, q rays per wave (64 / 2^ceil(log2 q) lanes per ray). */
+#define RTX_DEBUG_CULLED_COOP(q) (0xFFFFFF00u | (unsigned)(q))
 RTX_API int rtx_debug_hit_world_from(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                      float t_min, float t_max, uint32_t start_block,
                                      float *out);

@@ -521,12 +521,13 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
             const uint32_t b = 8 * g + j;
             float *gb = &L.bnd[32 * (size_t)g];
             if (b >= nblk) {  // past the last block: masked off by the kernel; flat height for a flat group
-                gb[8 + j] = 8 * g >= L.flat_lo ? flat_cy : 0.0f;
+                gb[8 + j] = 8 * g >= L.flat_lo ? rtx::kCullSy * flat_cy : 0.0f;
                 continue;
             }
             const float *sp[8];
             for (int i = 0; i < 8; ++i) sp[i] = &S[4 * (size_t)L.perm[8 * b + i]];
-            const rtx::CullBound cb = rtx::cull_bound(sp, 8, b >= L.flat_lo, flat_cy);
+            const bool fl = b >= L.flat_lo;  // flat: bounded in the space stretched along y
+            const rtx::CullBound cb = rtx::cull_bound(sp, 8, fl, flat_cy, fl ? rtx::kCullSy : 1.0f);
             gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
         }
     // the top level: one bound over each group's 64 spheres, 8 groups per super-group
@@ -538,12 +539,14 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
             const uint32_t g = 8 * s + j;
             float *gb = &L.bnd2[32 * (size_t)s];
             if (g >= ngrp) {
-                gb[8 + j] = 64 * s >= L.flat_lo ? flat_cy : 0.0f;
+                gb[8 + j] = 64 * s >= L.flat_lo ? rtx::kCullSy * flat_cy : 0.0f;
                 continue;
             }
             sp64.clear();
             for (uint32_t p = 64 * g; p < std::min(64 * g + 64, np); ++p) sp64.push_back(&S[4 * (size_t)L.perm[p]]);
-            const rtx::CullBound cb = rtx::cull_bound(sp64.data(), (int)sp64.size(), 8 * g >= L.flat_lo, flat_cy);
+            const bool fl = 8 * g >= L.flat_lo;
+            const rtx::CullBound cb =
+                rtx::cull_bound(sp64.data(), (int)sp64.size(), fl, flat_cy, fl ? rtx::kCullSy : 1.0f);
             gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
         }
     return L;

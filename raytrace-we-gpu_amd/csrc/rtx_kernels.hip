@@ -718,12 +718,17 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // the resolve maps them through cperm). Returns the block to resume at: the
 // end, or the block after the one at which some lane's list filled (a resumed
 // group is tested again, its earlier blocks masked off). Wave-uniform.
-__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, uint32_t *list,
-                                                uint32_t &cnt) {
+__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, const LineTest &Ts,
+                                                uint32_t *list, uint32_t &cnt) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
     const uint32_t nblk = S.n_cpad / 8u;
     const LineFlat K = line_test_flat(T, S.flat_cy);
+    // flat bounds: the ray stretched along y (rtx_prefilter.h kCullSy), the 5-op test
+    const LineFlat Ks = line_test_flat(Ts, kCullSy * S.flat_cy);
+    const f2v uxs = {Ts.ux, Ts.ux}, uzs = {Ts.uz, Ts.uz}, vzs = {Ts.vz, Ts.vz}, kus = {Ks.ku, Ks.ku},
+              kvs = {Ks.kv, Ks.kv};
+    const float thr_bs = Ts.thr * kCullThrScaleSy;
     f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
     f2v ku = {K.ku, K.ku}, kv = {K.kv, K.kv};
     const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
@@ -781,15 +786,25 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     using Flat = std::integral_constant<bool, true>;
     using Full = std::integral_constant<bool, false>;
     // the wave-OR of the 8 bound tests of an AoSoA-8 group of bounds: bit j
-    // when some lane's line passes bound j (8 ballots)
+    // when some lane's line passes bound j (8 ballots). Flat bounds are in
+    // the stretched space: the stretched ray's 5-op test against thr_bs.
     auto bound_mask = [&](cfloat_p grp, bool flat) -> uint32_t {
         float v[32];
         f2v q[4];
+        float thr = thr_b;
         if (flat) {
 #pragma unroll
             for (int i = 0; i < 32; ++i)
                 if (i < 8 || i >= 16) v[i] = grp[i];
-            quad(Flat(), [&](int i) { return v[i]; }, q);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const f2v cx = {v[2 * p], v[2 * p + 1]}, cz = {v[16 + 2 * p], v[17 + 2 * p]};
+                const f2v R = {v[24 + 2 * p], v[25 + 2 * p]};
+                const f2v pu = fma2(cx, uxs, fma2(cz, uzs, kus));
+                const f2v pv = fma2(cz, vzs, kvs);
+                q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+            }
+            thr = thr_bs;
         } else {
 #pragma unroll
             for (int i = 0; i < 32; ++i) v[i] = grp[i];
@@ -798,8 +813,8 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
         uint32_t m = 0;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            m |= (__ballot(!(q[p].x < thr_b)) != 0ull ? 1u : 0u) << (2 * p);
-            m |= (__ballot(!(q[p].y < thr_b)) != 0ull ? 1u : 0u) << (2 * p + 1);
+            m |= (__ballot(!(q[p].x < thr)) != 0ull ? 1u : 0u) << (2 * p);
+            m |= (__ballot(!(q[p].y < thr)) != 0ull ? 1u : 0u) << (2 * p + 1);
         }
         return m;
     };
@@ -835,9 +850,17 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
 // resolution rule is order-independent; the bounds never drop a reference
 // candidate). The resolve reads a candidate's (centre, radius) from ccen and
 // its scene index (the key's tie-break) from cperm, both by layout position.
+// The ray stretched along y for the flat bounds (rtx_prefilter.h kCullSy;
+// tests/prefilter_check.cpp runs the same ops).
+__device__ __forceinline__ LineTest line_test_stretched(const KScene &S, f3 o, f3 d) {
+    const float dys = kCullSy * d.y;
+    const float as = fmaf(d.z, d.z, fmaf(dys, dys, d.x * d.x));
+    return line_test_setup(o.x, kCullSy * o.y, o.z, d.x, dys, d.z, as, S.smag * kCullSy);
+}
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
                                                 float &best, uint32_t *list) {
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
+    const LineTest Ts = line_test_stretched(S, o, d);
     const float best0 = best;
     int idx = -1;
     bool ok = true;
@@ -847,7 +870,7 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = scan_culled(S, b, T, list, cnt);
+        b = scan_culled(S, b, T, Ts, list, cnt);
         ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
                                                               idx, cand_of<true>(), gi) &&
              ok;
@@ -1228,11 +1251,12 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
         const f3 ro = mk3(w[0], w[1], w[2]), rd = mk3(w[3], w[4], w[5]);
         const float ra = w[6], ria = w[7];
         const LineTest T = line_test_setup(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ra, S.smag);
-        const f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy}, vz = {T.vz, T.vz};
-        const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
-        const float thr_b = T.thr * kCullThrScale;
-        // bit j: entry j of an AoSoA-8 block (bounds or spheres) passes Q >= thr
-        auto block_mask = [&](const float *blk, float thr) -> uint32_t {
+        const LineTest Ts = line_test_stretched(S, ro, rd);  // the flat bounds' space (kCullSy)
+        const float thr_b = T.thr * kCullThrScale, thr_bs = Ts.thr * kCullThrScaleSy;
+        // bit j: entry j of an AoSoA-8 block (bounds or spheres) passes Q >= thr, the 7-op test of line L
+        auto block_mask = [&](const float *blk, const LineTest &L, float thr) -> uint32_t {
+            const f2v ux = {L.ux, L.ux}, uy = {L.uy, L.uy}, uz = {L.uz, L.uz}, vy = {L.vy, L.vy}, vz = {L.vz, L.vz};
+            const f2v nou = {L.nou, L.nou}, nov = {L.nov, L.nov};
             const float4 *b4 = reinterpret_cast<const float4 *>(blk);
             float4 v[8];
 #pragma unroll
@@ -1260,14 +1284,18 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
             const uint32_t gi = (st << lg) + k;
             if (gi >= ngrp) break;
             const float *gb = S.cbnd2 + 32u * (gi >> 3) + (gi & 7u);
-            if (line_test_q(T, gb[0], gb[8], gb[16], gb[24]) < thr_b) continue;
+            const bool flat = 8u * gi >= S.cflat_lo;  // the group's bound and its blocks' bounds are stretched
+            if (flat ? line_test_q(Ts, gb[0], gb[8], gb[16], gb[24]) < thr_bs
+                     : line_test_q(T, gb[0], gb[8], gb[16], gb[24]) < thr_b)
+                continue;
             const uint32_t left = nblk - 8u * gi;
-            uint32_t mb = block_mask(S.cbnd + 32u * gi, thr_b) & (left >= 8u ? 0xffu : (1u << left) - 1u);
+            uint32_t mb = (flat ? block_mask(S.cbnd + 32u * gi, Ts, thr_bs) : block_mask(S.cbnd + 32u * gi, T, thr_b)) &
+                          (left >= 8u ? 0xffu : (1u << left) - 1u);
 #pragma unroll 1
             while (mb != 0u) {
                 const uint32_t bb = 8u * gi + (uint32_t)__builtin_ctz(mb);
                 mb &= mb - 1u;
-                uint32_t ms = block_mask(S.cpre + 32u * bb, T.thr);
+                uint32_t ms = block_mask(S.cpre + 32u * bb, T, T.thr);
 #pragma unroll 1
                 while (ms != 0u) {
                     const uint32_t pos = 8u * bb + (uint32_t)__builtin_ctz(ms);
@@ -2915,6 +2943,28 @@ __global__ void __launch_bounds__(kBlock) k_unpermute(const float4 *__restrict__
     if (v.w != 0.0f) out[i] = v;
 }
 
+// One hit record of rtx_debug_hit_world (include/rtx.h): hit, t, p, normal,
+// front_face, sphere index.
+__device__ __forceinline__ void debug_record(const KScene &S, f3 o, f3 d, float best, int idx, float *r) {
+    if (idx < 0) {
+        for (int k = 0; k < 10; ++k) r[k] = 0.0f;
+        r[9] = -1.0f;
+        return;
+    }
+    const float4 sc = S.cen[idx];
+    const f3 p = o + best * d;
+    const float inv_r = 1.0f / sc.w;
+    f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));
+    const bool ff = dot3(d, nrm) < 0.0f;
+    if (!ff) nrm = -nrm;
+    r[0] = 1.0f;
+    r[1] = best;
+    r[2] = p.x; r[3] = p.y; r[4] = p.z;
+    r[5] = nrm.x; r[6] = nrm.y; r[7] = nrm.z;
+    r[8] = ff ? 1.0f : 0.0f;
+    r[9] = (float)idx;
+}
+
 // t_min > 0 and t_max >= t_min (rtx_debug_hit_world checks): the resolve
 // orders roots by their bits (hit_key). start = kDebugCulled: the culled
 // scan (k_render's lane mode for scenes with KScene::cpre), when the scene has it.
@@ -2937,24 +2987,39 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
             : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
                                    : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
-    float *r = out + 10 * (size_t)i;
-    if (idx < 0) {
-        for (int k = 0; k < 10; ++k) r[k] = 0.0f;
-        r[9] = -1.0f;
-        return;
+    debug_record(S, o, d, best, idx, out + 10 * (size_t)i);
+}
+
+// start = kDebugCulledCoop | q (q in 1..64): the culled group coop
+// (hit_world_groups_culled, the large-scene tail / heavy tiers) with q rays
+// per wave, i.e. 64 / 2^ceil(log2 q) lanes per ray (q > 32: two chunks of
+// 32 rays at 2 lanes each); a ray whose group met a non-finite root takes
+// the in-order path, as in the render.
+constexpr uint32_t kDebugCulledCoop = 0xffffff00u;
+__global__ void __launch_bounds__(kRB) k_debug_hit_world_coop(const KScene S, const float *rays, uint32_t nrays,
+                                                              float t_min, float t_max, uint32_t q, float *out) {
+    __shared__ uint32_t list[list_bytes<true>() / sizeof(uint32_t)];
+    __shared__ float ws_all[(kRB / 64) * (kCoopWaveBytes / 4)];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x / 64u;
+    const uint32_t i = (blockIdx.x * (kRB / 64u) + w) * q + lane;
+    const bool active = lane < q && i < nrays;
+    f3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(1.0f, 0.0f, 0.0f);
+    if (active) {
+        o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
+        d = mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     }
-    const float4 sc = S.cen[idx];
-    const f3 p = o + best * d;
-    const float inv_r = 1.0f / sc.w;
-    f3 nrm = inv_r * (p - mk3(sc.x, sc.y, sc.z));
-    const bool ff = dot3(d, nrm) < 0.0f;
-    if (!ff) nrm = -nrm;
-    r[0] = 1.0f;
-    r[1] = best;
-    r[2] = p.x; r[3] = p.y; r[4] = p.z;
-    r[5] = nrm.x; r[6] = nrm.y; r[7] = nrm.z;
-    r[8] = ff ? 1.0f : 0.0f;
-    r[9] = (float)idx;
+    const float a = dir_len2(d);
+    const float inv_a = 1.0f / a;
+    float best = t_max;
+    bool seq = false;
+    int idx = hit_world_groups_culled(S, __ballot(active), active, o, d, a, inv_a, t_min,
+                                      ws_all + w * (kCoopWaveBytes / 4), best, seq);
+    if (!active) return;
+    if (seq) {
+        best = t_max;
+        idx = hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list);
+    }
+    debug_record(S, o, d, best, min(idx, (int)S.n - 1), out + 10 * (size_t)i);
 }
 
 // Issue-rate probe of hit_world's own instruction mix (rtx_debug_scan_rate,
@@ -3328,6 +3393,13 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays, float t_min,
                                   float t_max, uint32_t start_block, float *out, hipStream_t stream) {
     if (nrays == 0) return hipSuccess;
+    const uint32_t q = start_block & 0xffu;
+    if ((start_block & ~0xffu) == kDebugCulledCoop && q >= 1u && q <= 64u && s.cpre) {
+        const uint32_t waves = ceil_div(nrays, q);
+        hipLaunchKernelGGL(k_debug_hit_world_coop, dim3(ceil_div(waves, kRB / 64u)), dim3(kRB), 0, stream, s, rays,
+                           nrays, t_min, t_max, q, out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
                        rays, nrays, t_min, t_max, start_block, out);
     return hipGetLastError();

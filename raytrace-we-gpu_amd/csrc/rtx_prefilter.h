@@ -181,13 +181,32 @@ RTX_HD float line_test_q_flat(const LineTest &T, const LineFlat &K, float cx, fl
 // near-tangent rays through random blocks.
 constexpr float kCullThrScale = 4.25f;
 constexpr double kCullK = 1.0 / 32.0;
+// Flat bounds (every sphere at height flat_cy: the scene's thin layer) are
+// tested in a space stretched along y by kCullSy: the ray (o, d) becomes
+// (ox, s oy, oz), (dx, s dy, dz) (exact in fp32: s is a power of two), the
+// bound's centre (cx, s cy, cz). A sphere of radius r becomes an ellipsoid
+// inside the sphere of radius s r, and a point p of the line at distance
+// dperp_i from c_i maps to a point of the stretched line at distance <=
+// s dperp_i from the stretched centre, so the derivation above holds with
+// |c_i - C_b| measured in the stretched space, sqrt(A_i) and sqrt(B) scaled
+// by s, and |o| <= |o'|: rho' = max_i (|A c_i - C'_b| + s sqrt(A_i)),
+// thr'_b = -(kPreMarginO + (1 + 1/k) 26u s^2) |o'|^2 - kPreFloor, which is
+// >= thr' * kCullThrScaleSy (1.6e-5 + 33 * 26u * 16 = 8.34e-4 <= 1.6e-5 * 53).
+// The layer's bounds become nearly spheres (the layer is ~0.4 thick, a
+// block 2 x 4 cells wide), and a line passing above a patch no longer passes
+// its bound: at C5 a wave's lines pass 2.0 % of the flat block bounds instead
+// of 4.6 % (tools/block_cull_sim.py on the sampled rays).
+constexpr float kCullSy = 4.0f;
+constexpr float kCullThrScaleSy = 53.0f;
 
 struct CullBound {
     float cx, cy, cz, R;
 };
 // Spheres (cx, cy, cz, r)[m] as uploaded; flat: every centre has height
 // flat_cy (the bound's centre takes it exactly, so the 5-op test applies).
-inline CullBound cull_bound(const float *const *sph, int m, bool flat, float flat_cy) {
+// sy: the stretch along y (1, or kCullSy for a flat bound: then the centre
+// returned is in the stretched space, cy = sy * flat_cy).
+inline CullBound cull_bound(const float *const *sph, int m, bool flat, float flat_cy, float sy = 1.0f) {
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < m; ++i)
         for (int k = 0; k < 3; ++k) {
@@ -196,17 +215,17 @@ inline CullBound cull_bound(const float *const *sph, int m, bool flat, float fla
         }
     CullBound b;
     b.cx = (float)(0.5 * (lo[0] + hi[0]));
-    b.cy = flat ? flat_cy : (float)(0.5 * (lo[1] + hi[1]));
+    b.cy = flat ? sy * flat_cy : (float)(sy * 0.5 * (lo[1] + hi[1]));
     b.cz = (float)(0.5 * (lo[2] + hi[2]));
     const double u = 5.9604644775390625e-08;
     double rho = 0.0;
     for (int i = 0; i < m; ++i) {
-        const double dx = (double)sph[i][0] - b.cx, dy = (double)sph[i][1] - b.cy, dz = (double)sph[i][2] - b.cz;
+        const double dx = (double)sph[i][0] - b.cx, dy = (double)sy * sph[i][1] - b.cy, dz = (double)sph[i][2] - b.cz;
         const double r = sph[i][3];
         const double c2 = (double)sph[i][0] * sph[i][0] + (double)sph[i][1] * sph[i][1] + (double)sph[i][2] * sph[i][2];
         const double A = r * r * (1.0 + 8.0 * u) + 27.0 * u * c2;
         // (double rounding of these few ops is ~1e-16 relative: the 1e-12 covers it)
-        rho = fmax(rho, (sqrt(dx * dx + dy * dy + dz * dz) + sqrt(A)) * (1.0 + 1e-12));
+        rho = fmax(rho, (sqrt(dx * dx + dy * dy + dz * dz) + (double)sy * sqrt(A)) * (1.0 + 1e-12));
     }
     const double cb2 = (double)b.cx * b.cx + (double)b.cy * b.cy + (double)b.cz * b.cz;
     const double R = (1.0 + kCullK) * rho * rho * (1.0 + kPreMarginR) + kPreMarginC * cb2 + (double)kPreFloor;

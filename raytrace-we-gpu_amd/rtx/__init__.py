@@ -29,6 +29,13 @@ RTX_OK = 0
 RTX_ERR_INCOMPLETE = -5  # a render launch left pixels unwritten (ABI 1.3)
 SCHEDULE_ABI = 140  # the rtx_schedule layout this module passes (ABI 1.4.0)
 DEBUG_CULLED = 0xFFFFFFFF  # rtx_debug_hit_world_from: the culled scan (include/rtx.h RTX_DEBUG_CULLED)
+
+
+def DEBUG_CULLED_COOP(q: int) -> int:
+    """rtx_debug_hit_world_from: the culled group coop, q rays per wave (RTX_DEBUG_CULLED_COOP)."""
+    if not 1 <= q <= 64:
+        raise ValueError("q must be in 1..64")
+    return 0xFFFFFF00 | q
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,

@@ -43,9 +43,11 @@ static float ref_disc(const float o[3], const float d[3], const float c[3], floa
 // The culled scan's block bounds (rtx_prefilter.h cull_bound): a block of 8
 // spheres (a cluster of extent 1e-2..1e2 x the largest radius around a centre
 // of magnitude 1e-2..1e4, radii 1/8..1 x r, a third of the blocks flat: one
-// centre height), a near-tangent line to one of them; whenever the
-// reference's disc of that sphere is >= 0 (or NaN), the block test must pass
-// (line_test_q / line_test_q_flat on the bound against thr * kCullThrScale).
+// centre height, bounded and tested in the space stretched along y by
+// kCullSy), a near-tangent line to one of them; whenever the reference's
+// disc of that sphere is >= 0 (or NaN), the block test must pass
+// (line_test_q, and for flat blocks also line_test_q_flat, on the bound
+// against thr * kCullThrScale, or thr' * kCullThrScaleSy for the stretched ray).
 static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
     for (long k = 0; k < n; ++k) {
         double cd[3], dir[3], e[3], t[3];
@@ -73,10 +75,12 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
         }
         const float *sp[8];
         for (int i = 0; i < 8; ++i) sp[i] = sph[i];
-        const rtx::CullBound b = rtx::cull_bound(sp, 8, flat, sph[0][1]);
+        // flat blocks are bounded and tested in the space stretched along y
+        const float sy = flat ? rtx::kCullSy : 1.0f;
+        const rtx::CullBound b = rtx::cull_bound(sp, 8, flat, sph[0][1], sy);
         // half the lines graze the sphere on its side away from the bound's
         // centre (the tightest case for the bound), the others at random
-        const double away[3] = {c[0] - (double)b.cx, c[1] - (double)b.cy, c[2] - (double)b.cz};
+        const double away[3] = {c[0] - (double)b.cx, c[1] - (double)b.cy / sy, c[2] - (double)b.cz};
         const double al = std::sqrt(away[0] * away[0] + away[1] * away[1] + away[2] * away[2]);
         if (uni() < 0.5 && al > 0.0) {
             for (int i = 0; i < 3; ++i) t[i] = away[i] / al;
@@ -108,8 +112,14 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
         if ((double)smag < sm) smag = std::nextafter(smag, INFINITY);
         for (int j = 0; j < 3; ++j) rtx::pf_host_ulp[j] = (int)(uni() * 3.0) - 1;
         const rtx::LineTest T = rtx::line_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, smag);
-        const float thr_b = T.thr * rtx::kCullThrScale;
-        const float q = flat ? rtx::line_test_q_flat(T, rtx::line_test_flat(T, b.cy), b.cx, b.cz, b.R)
+        // the stretched ray (the kernel's own ops: sy * o.y, sy * d.y, a from them, smag * sy)
+        const float d1s = sy * d[1];
+        const float as = fmaf(d[2], d[2], fmaf(d1s, d1s, d[0] * d[0]));
+        const rtx::LineTest Ts = rtx::line_test_setup(o[0], sy * o[1], o[2], d[0], d1s, d[2], as, smag * sy);
+        const float thr_b = flat ? Ts.thr * rtx::kCullThrScaleSy : T.thr * rtx::kCullThrScale;
+        // flat: both op orders (lane mode: the 5-op flat test; the group coop: the 7-op one)
+        const float q = flat ? std::fmin(rtx::line_test_q_flat(Ts, rtx::line_test_flat(Ts, b.cy), b.cx, b.cz, b.R),
+                                         rtx::line_test_q(Ts, b.cx, b.cy, b.cz, b.R))
                              : rtx::line_test_q(T, b.cx, b.cy, b.cz, b.R);
         const bool ref = !(ref_disc(o, d, c, -r2, a) < 0.0f);
         ref_pos += ref;
@@ -118,7 +128,7 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
                 std::fprintf(stderr, "BLOCK MISS c=(%.9g %.9g %.9g) r=%.9g o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) q=%.9g thr_b=%.9g\n",
                              c[0], c[1], c[2], c[3], o[0], o[1], o[2], d[0], d[1], d[2], q, thr_b);
         }
-        if (ref && T.thr != -INFINITY) {
+        if (ref && T.thr != -INFINITY && thr_b != -INFINITY) {
             // the line's estimated dperp_b^2 against the bound's inflated R_b - thr_b
             const double used = ((double)b.R - q) / ((double)b.R - thr_b);
             if (used > max_used) max_used = used;

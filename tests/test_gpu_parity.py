@@ -193,6 +193,35 @@ def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx, scan):
     assert (want[:, 0] == 1).mean() > 0.3
 
 
+@pytest.mark.parametrize("q", [1, 2, 5, 8, 17, 32, 64])
+def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
+    """The culled scan split over a wave's lanes (hit_world_groups_culled: the
+    large-scene frame tail, heavy tiers and promoted pixels), q rays per wave
+    (64 lanes per ray at q = 1 down to 2 at q = 32; q > 32 in two chunks): grazing rays
+    over a 2,504-sphere scene, aimed and random rays over a scene of
+    duplicated spheres (ties), bit for bit against the oracle."""
+    rng = np.random.default_rng(100 + q)
+    world = rtx.random_world(25, depth=1, spp=1)
+    rays = grazing_rays(world.spheres, 4000, rng, xaxis_frac=0.05)
+    gpu_ctx.upload_world(world)
+    got = gpu_ctx.debug_hit_world(rays, start_block=rtx.DEBUG_CULLED_COOP(q))
+    assert_bits_equal(got, oracle.hit_world_f32(world, rays), f"culled coop q={q}, grazing")
+    base = np.concatenate([rng.uniform(-20, 20, (900, 1)), rng.uniform(0, 2, (900, 1)),
+                           rng.uniform(-20, 20, (900, 1)), rng.uniform(0.2, 0.9, (900, 1))], 1)
+    sph = np.concatenate([base, base[::-1]]).astype(np.float32)
+    n = len(sph)
+    dup = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
+    gpu_ctx.upload_world(dup)
+    o = rng.uniform(-22, 22, (3000, 3))
+    d = (sph[rng.integers(0, n, 3000), :3] - o) + rng.normal(scale=0.1, size=(3000, 3))
+    rays = np.concatenate([np.concatenate([o, d], 1), rng.normal(size=(1000, 6)) * 10]).astype(np.float32)
+    want = oracle.hit_world_f32(dup, rays, 0.001)
+    got = gpu_ctx.debug_hit_world(rays, t_min=0.001, start_block=rtx.DEBUG_CULLED_COOP(q))
+    assert_bits_equal(got, want, f"culled coop q={q}, ties")
+    hit = want[:, 9] >= 0
+    assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
+
+
 @pytest.mark.parametrize("n", [1025, 1100, 1500, 4100, 12000])
 def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
     """The culled scan (DESIGN.md §3e "culled scan") on scenes across its size
