@@ -196,8 +196,14 @@ constexpr double kCullK = 1.0 / 32.0;
 // block 2 x 4 cells wide), and a line passing above a patch no longer passes
 // its bound: at C5 a wave's lines pass 2.0 % of the flat block bounds instead
 // of 4.6 % (tools/block_cull_sim.py on the sampled rays).
-constexpr float kCullSy = 4.0f;
-constexpr float kCullThrScaleSy = 53.0f;
+#ifndef RTX_CULL_SY  // the stretch (a power of two: the scaling is exact)
+#define RTX_CULL_SY 4
+#endif
+constexpr float kCullSy = (float)RTX_CULL_SY;
+static_assert(RTX_CULL_SY >= 1 && (RTX_CULL_SY & (RTX_CULL_SY - 1)) == 0, "the stretch is a power of two");
+// 1 + (1 + 1/k) 26u sy^2 / kPreMarginO, rounded up (53 at sy = 4)
+constexpr float kCullThrScaleSy =
+    (float)(int)(2.0 + (1.0 + 1.0 / kCullK) * 26.0 * 5.9604644775390625e-08 * RTX_CULL_SY * RTX_CULL_SY / 1.6e-5);
 
 struct CullBound {
     float cx, cy, cz, R;
