@@ -189,13 +189,16 @@ constexpr uint32_t kRB = 256;           // threads per render workgroup
                               // dwords to scratch) sit in per-segment and coop code, none in the scan loop
 #endif
 #define RTX_RENDER_BOUNDS __launch_bounds__(kRB, RTX_WAVES_PER_SIMD)
-// The large-scene chain kernels (kPF: candidate lists of RTX_CAND_PF entries
-// and a 1-KiB scan tile per wave, ~34 KB of LDS per workgroup) fit 4
-// workgroups per CU's 160 KB of LDS, i.e. 4 waves per SIMD whatever their
-// registers allow: compiled for 5 they spilled 134 VGPRs (200 B/lane of
-// scratch) and 180 SGPRs for occupancy they never get; for 4 they have 128.
+// The large-scene chain kernels (kPF). With the full scan (RTX_CULL=0: lists
+// of RTX_CAND_PF entries and a 1-KiB scan tile per wave, ~34 KB of LDS per
+// workgroup) 4 workgroups fit a CU's 160 KB of LDS, i.e. 4 waves per SIMD:
+// compiled for 5 they spilled 134 VGPRs for occupancy they never got, for 4
+// they had 128. The culled scan (no tile) is latency-bound and its two line
+// bases (the stretched one for flat bounds) spill 63 VGPRs at 128: compiled
+// for 3 waves (166 VGPRs, no spills) the C5 frame is 2.5 % faster than at 4
+// and writes no spill lines (R8u).
 #ifndef RTX_WAVES_PER_SIMD_PF
-#define RTX_WAVES_PER_SIMD_PF 4
+#define RTX_WAVES_PER_SIMD_PF (RTX_CULL ? 3 : 4)
 #endif
 #define RTX_RENDER_BOUNDS_T(kPF) __launch_bounds__(kRB, (kPF) ? RTX_WAVES_PER_SIMD_PF : RTX_WAVES_PER_SIMD)
 #ifndef RTX_PS_WAVES_PF  // the per-sample kernel's large-scene instance (A/B: 4 = 128 VGPRs)
