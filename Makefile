@@ -56,7 +56,7 @@ clean:
 # product path):
 #   stress - candidate lists of 1 entry and coop resolve rounds of one scan
 #            step, so every overflow, round and fallback path runs all the
-#            time, and a 20 ms promotion valve (the heartbeat keeps live
+#            time, and a 100 ms promotion valve (the heartbeat keeps live
 #            launches going) (tests/test_gpu_parity.py)
 #   prof   - per-section clock sums (tools/section_prof.py)
 #   ptime  - per-pixel start/end times (tools/pixel_timeline.py)
@@ -65,7 +65,7 @@ clean:
 # Ad-hoc A/B builds for tools/variant_bench.py:
 #   make adhoc V=name VFLAGS="-DRTX_...=..."   -> lib/variants/librtx_name.so
 VARIANTS := stress prof ptime cprof rays
-VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=2000000ull
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=10000000ull
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1

@@ -76,6 +76,7 @@ struct rtx_ctx {
     float *d_cpre = nullptr;
     float *d_cbnd = nullptr;
     float *d_cbnd2 = nullptr;
+    float *d_cbnd3 = nullptr;
     uint32_t *d_cperm = nullptr;
     float4 *d_ccen = nullptr;
     uint32_t n_cpad = 0, cflat_lo = 0;
@@ -149,9 +150,10 @@ void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_cpre);
     (void)hipFree(c->d_cbnd);
     (void)hipFree(c->d_cbnd2);
+    (void)hipFree(c->d_cbnd3);
     (void)hipFree(c->d_cperm);
     (void)hipFree(c->d_ccen);
-    c->d_cpre = c->d_cbnd = c->d_cbnd2 = nullptr;
+    c->d_cpre = c->d_cbnd = c->d_cbnd2 = c->d_cbnd3 = nullptr;
     c->d_cperm = nullptr;
     c->d_ccen = nullptr;
     c->n_cpad = c->cflat_lo = 0;
@@ -181,6 +183,7 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.cpre = c->d_cpre;
     s.cbnd = c->d_cbnd;
     s.cbnd2 = c->d_cbnd2;
+    s.cbnd3 = c->d_cbnd3;
     s.cperm = c->d_cperm;
     s.ccen = c->d_ccen;
     s.n_cpad = c->n_cpad;
@@ -463,7 +466,7 @@ int rtx_get_schedule(rtx_ctx *c, rtx_schedule *out) {
 // prefilter's safe region (thr = -inf flags everything), which then resolves
 // the copy to the same key as the sphere itself — no result changes either way.
 struct CullLayout {
-    std::vector<float> pre, bnd, bnd2;
+    std::vector<float> pre, bnd, bnd2, bnd3;
     std::vector<uint32_t> perm;
     std::vector<uint8_t> pad;  // position holds a padding copy
     uint32_t flat_lo = 0;
@@ -503,12 +506,30 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
         if (sec[k].empty()) continue;
         std::stable_sort(sec[k].begin(), sec[k].end(),
                          [&](uint32_t a, uint32_t b) { return morton(a, k == 2) < morton(b, k == 2); });
-        if (k == 2) L.flat_lo = (uint32_t)L.perm.size() / 8;
+        if (k == 2) {
+            // the flat section starts at a multiple of kCullAlign blocks, so
+            // that no bound test (8 entries of 1, 8 or 64 blocks) mixes flat
+            // and non-flat bounds; the padding blocks' bounds never pass (R = -inf)
+            while (!L.perm.empty() && (L.perm.size() / 8) % rtx::kCullAlign != 0) {
+                const uint32_t last = L.perm.back();
+                for (int i = 0; i < 8; ++i) L.perm.push_back(last), L.pad.push_back(1);
+            }
+            L.flat_lo = (uint32_t)L.perm.size() / 8;
+        }
         for (uint32_t i : sec[k]) L.perm.push_back(i), L.pad.push_back(0);
         while (L.perm.size() % 8) L.perm.push_back(sec[k].back()), L.pad.push_back(1);
     }
     if (sec[2].empty()) L.flat_lo = (uint32_t)L.perm.size() / 8;
     const uint32_t np = (uint32_t)L.perm.size(), nblk = np / 8, ngrp = (nblk + 7) / 8;
+    // the bound of positions [p0, p1): over their spheres; R = -inf when they are all padding
+    auto bound_of = [&](uint32_t p0, uint32_t p1, bool fl) {
+        std::vector<const float *> sp;
+        bool all_pad = true;
+        for (uint32_t p = p0; p < std::min(p1, np); ++p) sp.push_back(&S[4 * (size_t)L.perm[p]]), all_pad &= L.pad[p] != 0;
+        rtx::CullBound cb = rtx::cull_bound(sp.data(), (int)sp.size(), fl, flat_cy, fl ? rtx::kCullSy : 1.0f);
+        if (all_pad) cb.R = -INFINITY;
+        return cb;
+    };
     L.pre.assign(4 * (size_t)np, 0.0f);
     for (uint32_t p = 0; p < np; ++p) {
         const float4 v = pre4[L.perm[p]];
@@ -524,16 +545,12 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
                 gb[8 + j] = 8 * g >= L.flat_lo ? rtx::kCullSy * flat_cy : 0.0f;
                 continue;
             }
-            const float *sp[8];
-            for (int i = 0; i < 8; ++i) sp[i] = &S[4 * (size_t)L.perm[8 * b + i]];
-            const bool fl = b >= L.flat_lo;  // flat: bounded in the space stretched along y
-            const rtx::CullBound cb = rtx::cull_bound(sp, 8, fl, flat_cy, fl ? rtx::kCullSy : 1.0f);
+            const rtx::CullBound cb = bound_of(8 * b, 8 * b + 8, b >= L.flat_lo);  // flat: stretched along y
             gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
         }
     // the top level: one bound over each group's 64 spheres, 8 groups per super-group
     const uint32_t nsg = (ngrp + 7) / 8;
     L.bnd2.assign(32 * (size_t)nsg, 0.0f);
-    std::vector<const float *> sp64;
     for (uint32_t s = 0; s < nsg; ++s)
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t g = 8 * s + j;
@@ -542,11 +559,21 @@ static CullLayout build_cull(const rtx_world *w, const std::vector<float4> &pre4
                 gb[8 + j] = 64 * s >= L.flat_lo ? rtx::kCullSy * flat_cy : 0.0f;
                 continue;
             }
-            sp64.clear();
-            for (uint32_t p = 64 * g; p < std::min(64 * g + 64, np); ++p) sp64.push_back(&S[4 * (size_t)L.perm[p]]);
-            const bool fl = 8 * g >= L.flat_lo;
-            const rtx::CullBound cb =
-                rtx::cull_bound(sp64.data(), (int)sp64.size(), fl, flat_cy, fl ? rtx::kCullSy : 1.0f);
+            const rtx::CullBound cb = bound_of(64 * g, 64 * g + 64, 8 * g >= L.flat_lo);
+            gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
+        }
+    // the third level: one bound over each super-group's 512 spheres, 8 per entry of bnd3
+    const uint32_t nhg = (nsg + 7) / 8;
+    L.bnd3.assign(32 * (size_t)nhg, 0.0f);
+    for (uint32_t h = 0; h < nhg; ++h)
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t sg = 8 * h + j;
+            float *gb = &L.bnd3[32 * (size_t)h];
+            if (sg >= nsg) {
+                gb[8 + j] = 512 * h >= L.flat_lo ? rtx::kCullSy * flat_cy : 0.0f;
+                continue;
+            }
+            const rtx::CullBound cb = bound_of(512 * sg, 512 * sg + 512, 64 * sg >= L.flat_lo);
             gb[j] = cb.cx, gb[8 + j] = cb.cy, gb[16 + j] = cb.cz, gb[24 + j] = cb.R;
         }
     return L;
@@ -659,6 +686,9 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         RTX_HIP(hipMalloc(&c->d_cpre, cl.pre.size() * sizeof(float)));
         RTX_HIP(hipMalloc(&c->d_cbnd, cl.bnd.size() * sizeof(float)));
         RTX_HIP(hipMalloc(&c->d_cbnd2, cl.bnd2.size() * sizeof(float)));
+        RTX_HIP(hipMalloc(&c->d_cbnd3, cl.bnd3.size() * sizeof(float)));
+        RTX_HIP(hipMemcpyAsync(c->d_cbnd3, cl.bnd3.data(), cl.bnd3.size() * sizeof(float), hipMemcpyHostToDevice,
+                               c->stream));
         RTX_HIP(hipMemcpyAsync(c->d_cbnd2, cl.bnd2.data(), cl.bnd2.size() * sizeof(float), hipMemcpyHostToDevice,
                                c->stream));
         RTX_HIP(hipMalloc(&c->d_cperm, cl.perm.size() * sizeof(uint32_t)));

@@ -40,14 +40,19 @@ struct KScene {
     // each block's bounding sphere (rtx_prefilter.h cull_bound)
     //   cpre  float[n_cpad*4]  AoSoA-8 like pre (cx cy cz R), position order
     //   cbnd  float[ceil(n_cpad/64)*32]  AoSoA-8 groups of 8 block bounds (cx cy cz R_b)
-    //   cbnd2 float[ceil(n_cpad/512)*32] AoSoA-8 super-groups of 8 group bounds (each
-    //                          over the 64 spheres of a group of 8 blocks)
+    //   cbnd2 float[ceil(n_cpad/512)*32] AoSoA-8: per super-group (64 blocks) its 8 group
+    //                          bounds (each over the 64 spheres of a group of 8 blocks)
+    //   cbnd3 float[ceil(n_cpad/4096)*32] AoSoA-8: per 512 blocks the 8 super-group bounds
+    //                          (each over a super-group's 512 spheres)
+    // A bound is flat — stored in the space stretched along y (rtx_prefilter.h
+    // kCullSy) — iff its first block is >= cflat_lo.
     //   ccen  float4[n_cpad]   cen in position order (the resolve's sphere data)
     //   cperm uint32[n_cpad]   position -> scene index (a pad: a copy with R = -inf)
     // Blocks [cflat_lo, n_cpad/8) hold only spheres at height flat_cy.
     const float *cpre;
     const float *cbnd;
     const float *cbnd2;
+    const float *cbnd3;
     const float4 *ccen;
     const uint32_t *cperm;
     uint32_t n_cpad, cflat_lo;
@@ -56,6 +61,12 @@ struct KScene {
 #ifndef RTX_CULL  // A/B build: 0 = no culled layout (the large-scene lane-mode scan visits every block)
 #define RTX_CULL 1
 #endif
+#ifndef RTX_CULL_LEVELS  // bound levels above the blocks: 2 (groups, super-groups) or 3 (+ 512-block ranges)
+#define RTX_CULL_LEVELS 3
+#endif
+// the flat section of the culled layout starts at a multiple of this many
+// blocks: no bound test (8 entries) mixes flat and non-flat bounds
+constexpr uint32_t kCullAlign = RTX_CULL_LEVELS >= 3 ? 512u : 64u;
 #ifndef RTX_SCAN_PF_MIN  // (A/B builds: 0 sends every scene to the kPF kernels)
 #define RTX_SCAN_PF_MIN 1024
 #endif

@@ -791,7 +791,7 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     // the wave-OR of the 8 bound tests of an AoSoA-8 group of bounds: bit j
     // when some lane's line passes bound j (8 ballots). Flat bounds are in
     // the stretched space: the stretched ray's 5-op test against thr_bs.
-    auto bound_mask = [&](cfloat_p grp, bool flat) -> uint32_t {
+    auto bound_mask1 = [&](cfloat_p grp, bool flat) -> uint32_t {
         float v[32];
         f2v q[4];
         float thr = thr_b;
@@ -822,27 +822,37 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
         return m;
     };
     auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
-    // Two levels: a top bound covers the 64 spheres of a group of 8 blocks;
-    // the top bounds are tested 8 at a time (one "super-group": 64 blocks),
-    // then, for each passing group, its 8 block bounds, then the passing
-    // blocks' spheres. A resumed scan (b inside a super-group) masks off the
-    // groups and blocks before b.
-    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u;
-    for (uint32_t sg = b >> 6; sg < nsg; ++sg) {
-        uint32_t m2 = bound_mask((cfloat_p)S.cbnd2 + 32u * sg, 64u * sg >= S.cflat_lo);
-        m2 &= first_bits(ng - 8u * sg);
-        if (sg == (b >> 6)) m2 &= 0xffu << ((b >> 3) & 7u);
-        RTX_DIAG_ADD(6, (uint32_t)__popc(m2));
-        while (m2 != 0u) {
-            const uint32_t g = 8u * sg + (uint32_t)__builtin_ctz(m2);
-            m2 &= m2 - 1u;
-            uint32_t m = bound_mask((cfloat_p)S.cbnd + 32u * g, 8u * g >= S.cflat_lo);
-            m &= first_bits(nblk - 8u * g);
-            if (g == (b >> 3)) m &= 0xffu << (b & 7u);
-            while (m != 0u) {
-                const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
-                m &= m - 1u;
-                if (bb >= S.cflat_lo ? step(Flat(), bb) : step(Full(), bb)) return bb + 1u;
+    // 8 bounds whose entries cover blocks from b0 on: flat (stored and tested
+    // stretched) iff b0 >= cflat_lo (cflat_lo is a multiple of 512 blocks, so
+    // no test straddles it: rtx_api.hip build_cull)
+    auto bound_mask = [&](cfloat_p grp, uint32_t b0) -> uint32_t { return bound_mask1(grp, b0 >= S.cflat_lo); };
+    // Three levels above the blocks: a group bound covers the 64 spheres of 8
+    // blocks, a super bound the 512 of 8 groups; the super bounds are tested 8
+    // at a time (4,096 spheres), then, for each passing super-group, its 8
+    // group bounds, for each passing group its 8 block bounds, then the
+    // passing blocks' spheres. A resumed scan (b inside a range) masks off
+    // the super-groups, groups and blocks before b.
+    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u, nhg = (nsg + 7u) / 8u;
+    for (uint32_t hg = b >> 9; hg < nhg; ++hg) {
+        uint32_t m3 = first_bits(nsg - 8u * hg);
+        if (RTX_CULL_LEVELS >= 3) m3 &= bound_mask((cfloat_p)S.cbnd3 + 32u * hg, 512u * hg);
+        if (hg == (b >> 9)) m3 &= 0xffu << ((b >> 6) & 7u);
+        while (m3 != 0u) {
+            const uint32_t sg = 8u * hg + (uint32_t)__builtin_ctz(m3);
+            m3 &= m3 - 1u;
+            uint32_t m2 = bound_mask((cfloat_p)S.cbnd2 + 32u * sg, 64u * sg) & first_bits(ng - 8u * sg);
+            if (sg == (b >> 6)) m2 &= 0xffu << ((b >> 3) & 7u);
+            RTX_DIAG_ADD(6, (uint32_t)__popc(m2));
+            while (m2 != 0u) {
+                const uint32_t g = 8u * sg + (uint32_t)__builtin_ctz(m2);
+                m2 &= m2 - 1u;
+                uint32_t m = bound_mask((cfloat_p)S.cbnd + 32u * g, 8u * g) & first_bits(nblk - 8u * g);
+                if (g == (b >> 3)) m &= 0xffu << (b & 7u);
+                while (m != 0u) {
+                    const uint32_t bb = 8u * g + (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    if (bb >= S.cflat_lo ? step(Flat(), bb) : step(Full(), bb)) return bb + 1u;
+                }
             }
         }
     }
@@ -1281,29 +1291,39 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
         };
         uint64_t key = hit_key(inf, -1);
         bool ok = true;
-        const uint32_t nsteps = valid ? (ngrp + g - 1u) >> lg : 0u;
+        // 8 bounds whose entries cover blocks from b0 on (flat, i.e. stretched,
+        // iff b0 >= cflat_lo: no test straddles it)
+        auto bounds_mask = [&](const float *blk, uint32_t b0) -> uint32_t {
+            return b0 >= S.cflat_lo ? block_mask(blk, Ts, thr_bs) : block_mask(blk, T, thr_b);
+        };
+        auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
+        const uint32_t nsg = (ngrp + 7u) / 8u;
+        const uint32_t nsteps = valid ? (nsg + g - 1u) >> lg : 0u;
 #pragma unroll 1
         for (uint32_t st = 0; st < nsteps; ++st) {
-            const uint32_t gi = (st << lg) + k;
-            if (gi >= ngrp) break;
-            const float *gb = S.cbnd2 + 32u * (gi >> 3) + (gi & 7u);
-            const bool flat = 8u * gi >= S.cflat_lo;  // the group's bound and its blocks' bounds are stretched
-            if (flat ? line_test_q(Ts, gb[0], gb[8], gb[16], gb[24]) < thr_bs
-                     : line_test_q(T, gb[0], gb[8], gb[16], gb[24]) < thr_b)
+            const uint32_t si = (st << lg) + k;  // super-group si: its bound (512 spheres) in cbnd3
+            if (si >= nsg) break;
+            const float *sb = S.cbnd3 + 32u * (si >> 3) + (si & 7u);
+            if (RTX_CULL_LEVELS >= 3 && (64u * si >= S.cflat_lo ? line_test_q(Ts, sb[0], sb[8], sb[16], sb[24]) < thr_bs
+                                                                : line_test_q(T, sb[0], sb[8], sb[16], sb[24]) < thr_b))
                 continue;
-            const uint32_t left = nblk - 8u * gi;
-            uint32_t mb = (flat ? block_mask(S.cbnd + 32u * gi, Ts, thr_bs) : block_mask(S.cbnd + 32u * gi, T, thr_b)) &
-                          (left >= 8u ? 0xffu : (1u << left) - 1u);
+            uint32_t mg = bounds_mask(S.cbnd2 + 32u * si, 64u * si) & first_bits(ngrp - 8u * si);
 #pragma unroll 1
-            while (mb != 0u) {
-                const uint32_t bb = 8u * gi + (uint32_t)__builtin_ctz(mb);
-                mb &= mb - 1u;
-                uint32_t ms = block_mask(S.cpre + 32u * bb, T, T.thr);
+            while (mg != 0u) {
+                const uint32_t gi = 8u * si + (uint32_t)__builtin_ctz(mg);
+                mg &= mg - 1u;
+                uint32_t mb = bounds_mask(S.cbnd + 32u * gi, 8u * gi) & first_bits(nblk - 8u * gi);
 #pragma unroll 1
-                while (ms != 0u) {
-                    const uint32_t pos = 8u * bb + (uint32_t)__builtin_ctz(ms);
-                    ms &= ms - 1u;
-                    resolve_one(S.ccen[pos], (int)S.cperm[pos], true, ro, rd, ra, ria, t_min, key, ok);
+                while (mb != 0u) {
+                    const uint32_t bb = 8u * gi + (uint32_t)__builtin_ctz(mb);
+                    mb &= mb - 1u;
+                    uint32_t ms = block_mask(S.cpre + 32u * bb, T, T.thr);
+#pragma unroll 1
+                    while (ms != 0u) {
+                        const uint32_t pos = 8u * bb + (uint32_t)__builtin_ctz(ms);
+                        ms &= ms - 1u;
+                        resolve_one(S.ccen[pos], (int)S.cperm[pos], true, ro, rd, ra, ria, t_min, key, ok);
+                    }
                 }
             }
         }

@@ -318,7 +318,7 @@ class Context:
                  lib: Optional[C.CDLL] = None):
         self._lib = lib or load_library()
         h = C.c_void_p()
-        _check(self._lib.rtx_create(device, C.byref(h)), "rtx_create")
+        _check(self._lib.rtx_create(device, C.byref(h)), "rtx_create", self._lib)
         self._h = h
         self.device = device
         self.frame: Optional[rtx_frame] = None
@@ -347,17 +347,17 @@ class Context:
         """Launch on `stream` (a hipStream_t handle; 0 = HIP's null stream,
         i.e. torch's default stream); None = the context's own stream."""
         if stream is None:
-            _check(self._lib.rtx_use_own_stream(self._h), "rtx_use_own_stream")
+            _check(self._lib.rtx_use_own_stream(self._h), "rtx_use_own_stream", self._lib)
         else:
-            _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream)), "rtx_set_stream")
+            _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream)), "rtx_set_stream", self._lib)
 
     def upload_world(self, world: World):
         w = world.as_struct()
-        _check(self._lib.rtx_upload_world(self._h, C.byref(w)), "rtx_upload_world")
+        _check(self._lib.rtx_upload_world(self._h, C.byref(w)), "rtx_upload_world", self._lib)
         self.world = world
 
     def set_frame(self, frame: rtx_frame):
-        _check(self._lib.rtx_set_frame(self._h, C.byref(frame)), "rtx_set_frame")
+        _check(self._lib.rtx_set_frame(self._h, C.byref(frame)), "rtx_set_frame", self._lib)
         self.frame = frame
 
     def render_rows(self, tile_rows: int, part: int, nparts: int, d_out: Optional[int] = None):
@@ -365,11 +365,11 @@ class Context:
                                          C.c_void_p(d_out or 0)), "rtx_render_rows")
 
     def render(self):
-        _check(self._lib.rtx_render(self._h), "rtx_render")
+        _check(self._lib.rtx_render(self._h), "rtx_render", self._lib)
 
     def accumulate(self, reset: bool = False) -> int:
         """Progressive accumulation; returns frames accumulated."""
-        _check(self._lib.rtx_accumulate(self._h, 1 if reset else 0), "rtx_accumulate")
+        _check(self._lib.rtx_accumulate(self._h, 1 if reset else 0), "rtx_accumulate", self._lib)
         return int(self._lib.rtx_accumulated_frames(self._h))
 
     def deinterleave(self, d_gathered: int, width: int, height: int, tile_rows: int, nparts: int,
@@ -379,7 +379,7 @@ class Context:
                "rtx_deinterleave_rows")
 
     def sync(self):
-        _check(self._lib.rtx_sync(self._h), "rtx_sync")
+        _check(self._lib.rtx_sync(self._h), "rtx_sync", self._lib)
 
     def framebuffer_ptr(self) -> int:
         return int(self._lib.rtx_framebuffer(self._h) or 0)
@@ -387,7 +387,7 @@ class Context:
     def download(self) -> np.ndarray:
         f = self.frame
         out = np.empty((f.height, f.width, 4), np.float32)
-        _check(self._lib.rtx_download(self._h, _fptr(out), out.nbytes), "rtx_download")
+        _check(self._lib.rtx_download(self._h, _fptr(out), out.nbytes), "rtx_download", self._lib)
         return out
 
     def render_image(self) -> np.ndarray:
@@ -398,11 +398,11 @@ class Context:
         return DeviceArray(self, shape, dtype)
 
     def stats_reset(self):
-        _check(self._lib.rtx_stats_reset(self._h), "rtx_stats_reset")
+        _check(self._lib.rtx_stats_reset(self._h), "rtx_stats_reset", self._lib)
 
     def stats(self) -> rtx_stats:
         s = rtx_stats()
-        _check(self._lib.rtx_get_stats(self._h, C.byref(s)), "rtx_get_stats")
+        _check(self._lib.rtx_get_stats(self._h, C.byref(s)), "rtx_get_stats", self._lib)
         return s
 
     def set_schedule(self, schedule: Optional[rtx_schedule] = None, **fields):
@@ -454,7 +454,7 @@ class Context:
         """hit_world alone at the render's occupancy (rtx_debug_scan_rate):
         (launch ms, wave-segments)."""
         ms, ws = C.c_float(0.0), C.c_uint64(0)
-        _check(self._lib.rtx_debug_scan_rate(self._h, reps, C.byref(ms), C.byref(ws)), "rtx_debug_scan_rate")
+        _check(self._lib.rtx_debug_scan_rate(self._h, reps, C.byref(ms), C.byref(ws)), "rtx_debug_scan_rate", self._lib)
         return float(ms.value), int(ws.value)
 
     def debug_pixel_cost(self, spp: int = 0) -> np.ndarray:

@@ -974,11 +974,12 @@ def test_promotion_across_the_chip(request, oracle, rtx, ctx_name):
     producers and servers sit on all 8). The launch must complete (no
     RTX_ERR_INCOMPLETE from rtx_get_stats), rows bit-exact, and the segment
     count equal to an independent exact-grid pass's. Through the stress build
-    the promotion valve is 20 ms: the frame's last chains run
-    longer than that without another pixel finishing, so the launch
-    completes only if the tracing waves' heartbeat counts as progress (a
-    2 ms valve fired here in R7e while only full waves, which had not seen
-    the queue exhausted and did not beat yet, were tracing)."""
+    the promotion valve is 100 ms: the launch completes only if
+    the tracing waves' heartbeat counts as progress while no pixel finishes
+    (a 2 ms valve fired here in R7e while only full waves, which had not
+    seen the queue exhausted and did not beat yet, were tracing; a 20 ms one
+    fired once in R8x, on a frame whose kernels had not changed: the stress
+    build's slowest stretches are longer than that)."""
     gpu_ctx = request.getfixturevalue(ctx_name)
     W, H, T = 1280, 720, 5
     world = rtx.random_world(11, depth=50, spp=12)
