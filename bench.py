@@ -440,7 +440,7 @@ def launch_desc(n_spheres, spp, nparts, rng):
     if spp < 8 and rng == "chain":
         return "rtx_render_rows launch = k_render<false> (exact grid, one lane per pixel)"
     large = ((n_spheres + 7) // 8) * 8 > 1024  # kScanPfMin: the kPF kernels
-    scan = ("culled scan over a spatially ordered copy of the scene (group bounds, block bounds, spheres;"
+    scan = ("culled scan over a spatially ordered copy of the scene (bounds over 512, 64 and 8 spheres, then spheres;"
             " the coop tiers split the same hierarchy over a ray's lanes), candidate lists of 24"
             if large else "scalar-loaded scan, resolve from the block's LDS copy of the scene")
     if rng == "per-sample":
