@@ -2046,7 +2046,7 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
 // but live chain — a big scene, a high spp — never trips the valve however
 // long it runs without another pixel finishing; only a launch in
 // which nothing traces any more does. The stress build (make all) runs with
-// a 20 ms valve (a beat every 1.25 ms), so its GPU tests exercise exactly
+// a 100 ms valve (a beat every 6.25 ms), so its GPU tests exercise exactly
 // that.
 #ifndef RTX_PROM_VALVE_TICKS
 #define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s of s_memrealtime (100 MHz)
