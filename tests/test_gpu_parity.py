@@ -198,10 +198,12 @@ def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
     """The culled scan split over a wave's lanes (hit_world_groups_culled: the
     large-scene frame tail, heavy tiers and promoted pixels), q rays per wave
     (64 lanes per ray at q = 1 down to 2 at q = 32; q > 32 in two chunks): grazing rays
-    over a 2,504-sphere scene, aimed and random rays over a scene of
+    over a 2,504-sphere scene (its flat layer's radii 0.05..0.6), aimed and random rays over a scene of
     duplicated spheres (ties), bit for bit against the oracle."""
     rng = np.random.default_rng(100 + q)
     world = rtx.random_world(25, depth=1, spp=1)
+    layer = world.spheres[:, 1] == np.float32(0.2)  # the flat layer, with radii 0.05..0.6 instead of 0.2
+    world.spheres[layer, 3] = rng.uniform(0.05, 0.6, layer.sum()).astype(np.float32)
     rays = grazing_rays(world.spheres, 4000, rng, xaxis_frac=0.05)
     gpu_ctx.upload_world(world)
     got = gpu_ctx.debug_hit_world(rays, start_block=rtx.DEBUG_CULLED_COOP(q))
@@ -233,8 +235,9 @@ def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
     rng = np.random.default_rng(n)
     k = n // 3
     ext = 11.0 * np.sqrt(n / 486.0)  # the RTIOW density
+    # the flat run (one centre height) with radii 0.05..0.6: its bounds live in the stretched space
     flat = np.concatenate([rng.uniform(-ext, ext, (k, 1)), np.full((k, 1), 0.2), rng.uniform(-ext, ext, (k, 1)),
-                           np.full((k, 1), 0.2)], 1)
+                           rng.uniform(0.05, 0.6, (k, 1))], 1)
     big = np.array([[0, -1000, 0, 1000], [0, 1, 0, 1.0], [-4, 1, 0, 1.0], [4, 1, 0, 1.0]])
     m = n - k - len(big) - 8
     other = np.concatenate([rng.uniform(-ext, ext, (m, 1)), rng.uniform(0, 3, (m, 1)), rng.uniform(-ext, ext, (m, 1)),
