@@ -1227,6 +1227,7 @@ __device__ __forceinline__ int hit_world_groups(const KScene &S, const Src &src,
 // visits about one group per lane instead of scanning 1,563 spheres per
 // lane. Bounds and spheres use the 7-op test (the margins cover it on
 // flat blocks too, rtx_prefilter.h).
+template <bool kBfs = true>
 __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t act, bool active, f3 o, f3 d,
                                                        float a, float inv_a, float t_min, float *ws, float &best,
                                                        bool &seq) {
@@ -1298,6 +1299,64 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
         };
         auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
         const uint32_t nsg = (ngrp + 7u) / 8u;
+        if (kBfs && m == 1u && RTX_CULL_BFS) {
+            // One ray, the whole wave: breadth first. Each level's passing
+            // entries are expanded 8 at a time, one child per lane (entry e's
+            // bound at (AoSoA-8) floats 32 (e >> 3) + (e & 7) + {0, 8, 16, 24}),
+            // so a level costs one round of loads for the wave instead of a
+            // lane walking its subtree load after dependent load.
+            auto test_entry = [&](const float *arr, uint32_t e, bool flat, float thr_flat, float thr_full) {
+                const float *q = arr + 32u * (e >> 3) + (e & 7u);
+                return flat ? !(line_test_q(Ts, q[0], q[8], q[16], q[24]) < thr_flat)
+                            : !(line_test_q(T, q[0], q[8], q[16], q[24]) < thr_full);
+            };
+            // the child this lane takes: of the (lane >> 3)-th set bit of the
+            // uniform mask m (the next 8 set bits are consumed)
+            auto take8 = [&](uint64_t &mm, uint32_t &parent) -> bool {
+                uint32_t sel = ~0u;
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint32_t bit = mm != 0ull ? (uint32_t)__builtin_ctzll(mm) : ~0u;
+                    if (mm != 0ull) mm &= mm - 1ull;
+                    if ((lane >> 3) == j) sel = bit;
+                }
+                parent = sel;
+                return sel != ~0u;
+            };
+#pragma unroll 1
+            for (uint32_t base = 0; base < nsg; base += 64u) {
+                const uint32_t si = base + lane;
+                uint64_t m3 = __ballot(si < nsg && (RTX_CULL_LEVELS < 3 ||
+                                                    test_entry(S.cbnd3, si, 64u * si >= S.cflat_lo, thr_bs, thr_b)));
+#pragma unroll 1
+                while (m3 != 0ull) {
+                    uint32_t ps;
+                    const bool h3 = take8(m3, ps);
+                    const uint32_t gi = h3 ? 8u * (base + ps) + (lane & 7u) : 0u;
+                    uint64_t m2 = __ballot(h3 && gi < ngrp &&
+                                           test_entry(S.cbnd2, gi, 8u * gi >= S.cflat_lo, thr_bs, thr_b));
+#pragma unroll 1
+                    while (m2 != 0ull) {
+                        uint32_t pg;
+                        const bool h2 = take8(m2, pg);
+                        // pg: a lane index of the level above, i.e. group 8 (base + ps') + (pg & 7) of that lane's
+                        // super-group: recover the group from the lane that tested it
+                        const uint32_t gsel = (uint32_t)__shfl((int)gi, (int)(h2 ? pg : 0u), 64);
+                        const uint32_t bb = h2 ? 8u * gsel + (lane & 7u) : 0u;
+                        uint64_t m1 = __ballot(h2 && bb < nblk && test_entry(S.cbnd, bb, bb >= S.cflat_lo, thr_bs, thr_b));
+#pragma unroll 1
+                        while (m1 != 0ull) {
+                            uint32_t pb;
+                            const bool h1 = take8(m1, pb);
+                            const uint32_t bsel = (uint32_t)__shfl((int)bb, (int)(h1 ? pb : 0u), 64);
+                            const uint32_t pos = h1 ? 8u * bsel + (lane & 7u) : 0u;
+                            const bool fl = h1 && test_entry(S.cpre, pos, false, T.thr, T.thr);
+                            if (fl) resolve_one(S.ccen[pos], (int)S.cperm[pos], true, ro, rd, ra, ria, t_min, key, ok);
+                        }
+                    }
+                }
+            }
+        } else {
         const uint32_t nsteps = valid ? (nsg + g - 1u) >> lg : 0u;
 #pragma unroll 1
         for (uint32_t st = 0; st < nsteps; ++st) {
@@ -1326,6 +1385,7 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
                     }
                 }
             }
+        }
         }
         // the group's (min c, then the largest index among equal c)
         const uint32_t cb0 = (uint32_t)(key >> 32);
@@ -2876,8 +2936,9 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
         if (exhausted && __popcll(act) <= kCoopMax) {  // the wave's last few samples: group coop
             __builtin_amdgcn_s_setprio(kTailPrio);
             bool seq = false;
-            hit = (kPF && RTX_CULL)
-                      ? hit_world_groups_culled(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best, seq)
+            hit = (kPF && RTX_CULL)  // (no breadth-first one-ray walk here: its registers cost this kernel 16 %, R9f)
+                      ? hit_world_groups_culled<false>(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws,
+                                                       best, seq)
                   : sph_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
                                                seq)
                             : hit_world_groups(P.scene, sg, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
