@@ -224,6 +224,31 @@ def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
     assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
 
 
+@pytest.mark.parametrize("layout", ["all_flat", "no_flat"])
+def test_hit_world_culled_scan_sections(gpu_ctx, oracle, rtx, layout):
+    """The culled layout's edge cases: a scene that is one flat layer but for
+    the ground sphere (the flat section after one padded block), and one with
+    no two centres at the same height (no flat section, nothing stretched)."""
+    rng = np.random.default_rng(5 if layout == "all_flat" else 6)
+    n = 3000
+    ext = 11.0 * np.sqrt(n / 486.0)
+    y = np.full((n - 1, 1), 0.2) if layout == "all_flat" else rng.uniform(0, 3, (n - 1, 1))
+    small = np.concatenate([rng.uniform(-ext, ext, (n - 1, 1)), y, rng.uniform(-ext, ext, (n - 1, 1)),
+                            rng.uniform(0.05, 0.5, (n - 1, 1))], 1)
+    sph = np.concatenate([[[0, -1000, 0, 1000]], small]).astype(np.float32)
+    world = rtx.World(sph, np.zeros(n, np.float32), np.zeros((n, 4), np.float32), 1, 1)
+    gpu_ctx.upload_world(world)
+    o = rng.uniform(-ext, ext, (5000, 3)) * np.array([1, 0.2, 1]) + np.array([0, 4, 0])
+    d = (sph[rng.integers(1, n, 5000), :3] - o) + rng.normal(scale=0.2, size=(5000, 3))
+    rays = np.concatenate([np.concatenate([o, d], 1), grazing_rays(sph[1:], 5000, rng, xaxis_frac=0.05)])
+    rays = rays.astype(np.float32)
+    want = oracle.hit_world_f32(world, rays)
+    for start, what in ((rtx.DEBUG_CULLED, "lane"), (rtx.DEBUG_CULLED_COOP(1), "coop 1"),
+                        (rtx.DEBUG_CULLED_COOP(8), "coop 8")):
+        assert_bits_equal(gpu_ctx.debug_hit_world(rays, start_block=start), want, f"{layout}, {what}")
+    assert (want[:, 0] == 1).mean() > 0.4
+
+
 @pytest.mark.parametrize("n", [1025, 1100, 1500, 4100, 12000])
 def test_hit_world_culled_scan(gpu_ctx, oracle, rtx, n):
     """The culled scan (DESIGN.md §3e "culled scan") on scenes across its size
