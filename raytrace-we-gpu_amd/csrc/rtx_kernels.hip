@@ -721,8 +721,11 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // the resolve maps them through cperm). Returns the block to resume at: the
 // end, or the block after the one at which some lane's list filled (a resumed
 // group is tested again, its earlier blocks masked off). Wave-uniform.
+// A bound also fails when it is wholly behind the lane's origin (the half
+// test H, Hs: rtx_prefilter.h HalfTest; 5 more fp32 ops per bound, 4 flat).
 __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, const LineTest &Ts,
-                                                uint32_t *list, uint32_t &cnt) {
+                                                const HalfTest &H, const HalfTest &Hs, uint32_t *list,
+                                                uint32_t &cnt) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
     const uint32_t nblk = S.n_cpad / 8u;
@@ -737,6 +740,10 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov};
     const f2v th = {T.thr, T.thr};
     const float thr_b = T.thr * kCullThrScale;
+    const f2v hdx = {H.dx, H.dx}, hdy = {H.dy, H.dy}, hdz = {H.dz, H.dz}, hnod = {H.nod, H.nod};
+    const f2v ha = {H.a, H.a}, htha = {H.tha, H.tha};
+    const float kws1 = half_test_kw(Hs, kCullSy * S.flat_cy);
+    const f2v kws = {kws1, kws1}, has = {Hs.a, Hs.a}, hthas = {Hs.tha, Hs.tha};
     // Q of the 4 pairs of an AoSoA-8 block of spheres or bounds (blk(i): its i-th float)
     auto quad = [&](auto flat, auto blk, f2v *q) {
 #pragma unroll
@@ -791,9 +798,11 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     // the wave-OR of the 8 bound tests of an AoSoA-8 group of bounds: bit j
     // when some lane's line passes bound j (8 ballots). Flat bounds are in
     // the stretched space: the stretched ray's 5-op test against thr_bs.
+    // A lane passes a bound when its line passes it and the bound is not
+    // wholly behind its origin (the half test; stretched for flat bounds).
     auto bound_mask1 = [&](cfloat_p grp, bool flat) -> uint32_t {
         float v[32];
-        f2v q[4];
+        f2v q[4], pw[4], q2[4];
         float thr = thr_b;
         if (flat) {
 #pragma unroll
@@ -806,18 +815,29 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
                 const f2v pu = fma2(cx, uxs, fma2(cz, uzs, kus));
                 const f2v pv = fma2(cz, vzs, kvs);
                 q[p] = fma2(-pv, pv, fma2(-pu, pu, R));
+                pw[p] = fma2(cx, hdx, fma2(cz, hdz, kws));
+                q2[p] = fma2(-pw[p], pw[p], fma2(R, has, hthas));
             }
             thr = thr_bs;
         } else {
 #pragma unroll
             for (int i = 0; i < 32; ++i) v[i] = grp[i];
             quad(Full(), [&](int i) { return v[i]; }, q);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const f2v cx = {v[2 * p], v[2 * p + 1]}, cy = {v[8 + 2 * p], v[9 + 2 * p]};
+                const f2v cz = {v[16 + 2 * p], v[17 + 2 * p]}, R = {v[24 + 2 * p], v[25 + 2 * p]};
+                pw[p] = fma2(cx, hdx, fma2(cy, hdy, fma2(cz, hdz, hnod)));
+                q2[p] = fma2(-pw[p], pw[p], fma2(R, ha, htha));
+            }
         }
         uint32_t m = 0;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            m |= (__ballot(!(q[p].x < thr)) != 0ull ? 1u : 0u) << (2 * p);
-            m |= (__ballot(!(q[p].y < thr)) != 0ull ? 1u : 0u) << (2 * p + 1);
+            const bool px = !(q[p].x < thr) && (!RTX_CULL_HALF || half_test_pass(pw[p].x, q2[p].x));
+            const bool py = !(q[p].y < thr) && (!RTX_CULL_HALF || half_test_pass(pw[p].y, q2[p].y));
+            m |= (__ballot(px) != 0ull ? 1u : 0u) << (2 * p);
+            m |= (__ballot(py) != 0ull ? 1u : 0u) << (2 * p + 1);
         }
         return m;
     };
@@ -870,10 +890,18 @@ __device__ __forceinline__ LineTest line_test_stretched(const KScene &S, f3 o, f
     const float as = fmaf(d.z, d.z, fmaf(dys, dys, d.x * d.x));
     return line_test_setup(o.x, kCullSy * o.y, o.z, d.x, dys, d.z, as, S.smag * kCullSy);
 }
+// The half test of the stretched ray (the same as, a, as line_test_stretched).
+__device__ __forceinline__ HalfTest half_test_stretched(f3 o, f3 d, float thr_bs, float t_min) {
+    const float dys = kCullSy * d.y;
+    const float as = fmaf(d.z, d.z, fmaf(dys, dys, d.x * d.x));
+    return half_test_setup(o.x, kCullSy * o.y, o.z, d.x, dys, d.z, as, thr_bs, t_min);
+}
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
                                                 float &best, uint32_t *list) {
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const LineTest Ts = line_test_stretched(S, o, d);
+    const HalfTest H = half_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, T.thr * kCullThrScale, t_min);
+    const HalfTest Hs = half_test_stretched(o, d, Ts.thr * kCullThrScaleSy, t_min);
     const float best0 = best;
     int idx = -1;
     bool ok = true;
@@ -883,7 +911,7 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     uint32_t b = 0;
     do {
         uint32_t cnt;
-        b = scan_culled(S, b, T, Ts, list, cnt);
+        b = scan_culled(S, b, T, Ts, H, Hs, list, cnt);
         ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
                                                               idx, cand_of<true>(), gi) &&
              ok;
@@ -1267,8 +1295,12 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
         const LineTest T = line_test_setup(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ra, S.smag);
         const LineTest Ts = line_test_stretched(S, ro, rd);  // the flat bounds' space (kCullSy)
         const float thr_b = T.thr * kCullThrScale, thr_bs = Ts.thr * kCullThrScaleSy;
-        // bit j: entry j of an AoSoA-8 block (bounds or spheres) passes Q >= thr, the 7-op test of line L
-        auto block_mask = [&](const float *blk, const LineTest &L, float thr) -> uint32_t {
+        const HalfTest H = half_test_setup(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ra, thr_b, t_min);
+        const HalfTest Hs = half_test_stretched(ro, rd, thr_bs, t_min);
+        // bit j: entry j of an AoSoA-8 block (bounds or spheres) passes Q >= thr, the 7-op test of line L;
+        // for bounds (Hh) also the half test
+        auto block_mask = [&](const float *blk, const LineTest &L, float thr,
+                              const HalfTest *Hh = nullptr) -> uint32_t {
             const f2v ux = {L.ux, L.ux}, uy = {L.uy, L.uy}, uz = {L.uz, L.uz}, vy = {L.vy, L.vy}, vz = {L.vz, L.vz};
             const f2v nou = {L.nou, L.nou}, nov = {L.nov, L.nov};
             const float4 *b4 = reinterpret_cast<const float4 *>(blk);
@@ -1285,17 +1317,35 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
                 const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
                 const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
                 const f2v q = fma2(-pv, pv, fma2(-pu, pu, R));
-                msk |= (!(q.x < thr) ? 1u : 0u) << (2 * p);
-                msk |= (!(q.y < thr) ? 1u : 0u) << (2 * p + 1);
+                bool px = !(q.x < thr), py = !(q.y < thr);
+                if (RTX_CULL_HALF && Hh) {
+                    const f2v hdx = {Hh->dx, Hh->dx}, hdy = {Hh->dy, Hh->dy}, hdz = {Hh->dz, Hh->dz};
+                    const f2v hnod = {Hh->nod, Hh->nod}, ha = {Hh->a, Hh->a}, htha = {Hh->tha, Hh->tha};
+                    const f2v pw = fma2(cx, hdx, fma2(cy, hdy, fma2(cz, hdz, hnod)));
+                    const f2v q2 = fma2(-pw, pw, fma2(R, ha, htha));
+                    px = px && half_test_pass(pw.x, q2.x);
+                    py = py && half_test_pass(pw.y, q2.y);
+                }
+                msk |= (px ? 1u : 0u) << (2 * p);
+                msk |= (py ? 1u : 0u) << (2 * p + 1);
             }
             return msk;
+        };
+        // one bound (7-op order), line and half test
+        auto bound_pass = [&](const float *q, bool flat) -> bool {
+            const LineTest &L = flat ? Ts : T;
+            const HalfTest &Hh = flat ? Hs : H;
+            if (line_test_q(L, q[0], q[8], q[16], q[24]) < (flat ? thr_bs : thr_b)) return false;
+            if (!RTX_CULL_HALF) return true;
+            const float pw = half_test_pw(Hh, q[0], q[8], q[16]);
+            return half_test_pass(pw, half_test_q2(Hh, pw, q[24]));
         };
         uint64_t key = hit_key(inf, -1);
         bool ok = true;
         // 8 bounds whose entries cover blocks from b0 on (flat, i.e. stretched,
         // iff b0 >= cflat_lo: no test straddles it)
         auto bounds_mask = [&](const float *blk, uint32_t b0) -> uint32_t {
-            return b0 >= S.cflat_lo ? block_mask(blk, Ts, thr_bs) : block_mask(blk, T, thr_b);
+            return b0 >= S.cflat_lo ? block_mask(blk, Ts, thr_bs, &Hs) : block_mask(blk, T, thr_b, &H);
         };
         auto first_bits = [](uint32_t n) { return n >= 8u ? 0xffu : (1u << n) - 1u; };
         const uint32_t nsg = (ngrp + 7u) / 8u;
@@ -1305,10 +1355,12 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
             // bound at (AoSoA-8) floats 32 (e >> 3) + (e & 7) + {0, 8, 16, 24}),
             // so a level costs one round of loads for the wave instead of a
             // lane walking its subtree load after dependent load.
-            auto test_entry = [&](const float *arr, uint32_t e, bool flat, float thr_flat, float thr_full) {
-                const float *q = arr + 32u * (e >> 3) + (e & 7u);
-                return flat ? !(line_test_q(Ts, q[0], q[8], q[16], q[24]) < thr_flat)
-                            : !(line_test_q(T, q[0], q[8], q[16], q[24]) < thr_full);
+            auto test_entry = [&](const float *arr, uint32_t e, bool flat) {
+                return bound_pass(arr + 32u * (e >> 3) + (e & 7u), flat);
+            };
+            auto test_sphere = [&](uint32_t pos) {
+                const float *q = S.cpre + 32u * (pos >> 3) + (pos & 7u);
+                return !(line_test_q(T, q[0], q[8], q[16], q[24]) < T.thr);
             };
             // the child this lane takes: of the (lane >> 3)-th set bit of the
             // uniform mask m (the next 8 set bits are consumed)
@@ -1327,14 +1379,14 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
             for (uint32_t base = 0; base < nsg; base += 64u) {
                 const uint32_t si = base + lane;
                 uint64_t m3 = __ballot(si < nsg && (RTX_CULL_LEVELS < 3 ||
-                                                    test_entry(S.cbnd3, si, 64u * si >= S.cflat_lo, thr_bs, thr_b)));
+                                                    test_entry(S.cbnd3, si, 64u * si >= S.cflat_lo)));
 #pragma unroll 1
                 while (m3 != 0ull) {
                     uint32_t ps;
                     const bool h3 = take8(m3, ps);
                     const uint32_t gi = h3 ? 8u * (base + ps) + (lane & 7u) : 0u;
                     uint64_t m2 = __ballot(h3 && gi < ngrp &&
-                                           test_entry(S.cbnd2, gi, 8u * gi >= S.cflat_lo, thr_bs, thr_b));
+                                           test_entry(S.cbnd2, gi, 8u * gi >= S.cflat_lo));
 #pragma unroll 1
                     while (m2 != 0ull) {
                         uint32_t pg;
@@ -1343,14 +1395,14 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
                         // super-group: recover the group from the lane that tested it
                         const uint32_t gsel = (uint32_t)__shfl((int)gi, (int)(h2 ? pg : 0u), 64);
                         const uint32_t bb = h2 ? 8u * gsel + (lane & 7u) : 0u;
-                        uint64_t m1 = __ballot(h2 && bb < nblk && test_entry(S.cbnd, bb, bb >= S.cflat_lo, thr_bs, thr_b));
+                        uint64_t m1 = __ballot(h2 && bb < nblk && test_entry(S.cbnd, bb, bb >= S.cflat_lo));
 #pragma unroll 1
                         while (m1 != 0ull) {
                             uint32_t pb;
                             const bool h1 = take8(m1, pb);
                             const uint32_t bsel = (uint32_t)__shfl((int)bb, (int)(h1 ? pb : 0u), 64);
                             const uint32_t pos = h1 ? 8u * bsel + (lane & 7u) : 0u;
-                            const bool fl = h1 && test_entry(S.cpre, pos, false, T.thr, T.thr);
+                            const bool fl = h1 && test_sphere(pos);
                             if (fl) resolve_one(S.ccen[pos], (int)S.cperm[pos], true, ro, rd, ra, ria, t_min, key, ok);
                         }
                     }
@@ -1363,9 +1415,7 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
             const uint32_t si = (st << lg) + k;  // super-group si: its bound (512 spheres) in cbnd3
             if (si >= nsg) break;
             const float *sb = S.cbnd3 + 32u * (si >> 3) + (si & 7u);
-            if (RTX_CULL_LEVELS >= 3 && (64u * si >= S.cflat_lo ? line_test_q(Ts, sb[0], sb[8], sb[16], sb[24]) < thr_bs
-                                                                : line_test_q(T, sb[0], sb[8], sb[16], sb[24]) < thr_b))
-                continue;
+            if (RTX_CULL_LEVELS >= 3 && !bound_pass(sb, 64u * si >= S.cflat_lo)) continue;
             uint32_t mg = bounds_mask(S.cbnd2 + 32u * si, 64u * si) & first_bits(ngrp - 8u * si);
 #pragma unroll 1
             while (mg != 0u) {

@@ -205,6 +205,53 @@ static_assert(RTX_CULL_SY >= 1 && (RTX_CULL_SY & (RTX_CULL_SY - 1)) == 0, "the s
 constexpr float kCullThrScaleSy =
     (float)(int)(2.0 + (1.0 + 1.0 / kCullK) * 26.0 * 5.9604644775390625e-08 * RTX_CULL_SY * RTX_CULL_SY / 1.6e-5);
 
+// Half-space part of the bound test. The line test above passes bounds the
+// ray's LINE passes, also those wholly behind the origin. The reference
+// accepts sphere i only at a root c >= t_min >= 0 (ShaderCompute.hlsl:
+// 160-166; oracle hit_world32), and then some point p = o + t d, t >= 0,
+// lies within sqrt(A_i + B) (1 + u) of c_i:
+//   near root accepted  ==>  fl(-hb - sq) >= 0  ==>  hb_c <= 0, and
+//     dot(c - o, d) >= -5u |c - o| |d|: the line's closest point (if t0 >= 0)
+//     or o itself (t0 in [-5u|c-o|/|d|, 0)) is within dperp_i (1 + u);
+//   far root accepted with hb_c > 0  ==>  disc_c >= hb_c^2 (1 - 2u)  ==>
+//     |o - c|^2 <= r^2 (1 + 16u): o itself, inside sqrt(A_i) (1 + 2u);
+// dperp_i^2 <= A_i + B as above. So |p - C_b| <= rho + sqrt(B) (1 + 2u) and
+//   pw = dot(C_b - o, d) = dot(C_b - p, d) + t a >= -(rho + sqrt(B)(1+2u)) |d|.
+// The kernel's pw_c = fl(C.d - o.d) is within e|d|, e = 4.2u (|C_b| + |o|),
+// and pw_c^2 <= ((1+k) rho^2 + (1+1/k)(1.1 B + 11 e^2)) a whenever pw_c < 0;
+// K = fl(fma(R_b, a, fl(-2 thr_b a))) exceeds that: R_b holds (1+k) rho^2
+// (1 + 2e-6) and 1.6e-5 |C_b|^2, and -2 thr_b >= 2 (6.71e-5 |o|^2) covers
+// (1 + 1/k) 1.1 B = 5.6e-5 |o|^2 (stretched: 2 * 8.48e-4 |o'|^2 against
+// 33 * 1.1 * 16 * 26u = 9.0e-4 |o'|^2, the proof carrying over as for the
+// line test: S p = S o + t S d is a point of the stretched ray). A bound
+// fails the half test iff pw_c < 0 and fl(fma(-pw_c, pw_c, K)) < 0; NaN
+// passes; thr_b = -inf (a lane outside the safe range) and t_min < 0 make
+// K = +inf: every bound passes. Checked with the line test by
+// tests/prefilter_check.cpp (block cases: reference acceptance at t_min 0
+// and 1e-3, origins on and inside the sphere, spheres behind the origin).
+struct HalfTest {
+    float dx, dy, dz, nod, a, tha;
+};
+RTX_HD HalfTest half_test_setup(float ox, float oy, float oz, float dx, float dy, float dz, float a, float thr_b,
+                                float t_min) {
+    HalfTest H;
+    H.dx = dx, H.dy = dy, H.dz = dz, H.a = a;
+    H.nod = -fmaf(oz, dz, fmaf(oy, dy, ox * dx));
+    const float th = (-2.0f * thr_b) * a;
+    H.tha = t_min >= 0.0f ? th : INFINITY;
+    return H;
+}
+// the 7-op order (c.d first), and the flat order (cy's term per ray: kw)
+RTX_HD float half_test_pw(const HalfTest &H, float cx, float cy, float cz) {
+    return fmaf(cx, H.dx, fmaf(cy, H.dy, fmaf(cz, H.dz, H.nod)));
+}
+RTX_HD float half_test_kw(const HalfTest &H, float cy) { return fmaf(cy, H.dy, H.nod); }
+RTX_HD float half_test_pw_flat(const HalfTest &H, float kw, float cx, float cz) {
+    return fmaf(cx, H.dx, fmaf(cz, H.dz, kw));
+}
+RTX_HD float half_test_q2(const HalfTest &H, float pw, float R) { return fmaf(-pw, pw, fmaf(R, H.a, H.tha)); }
+RTX_HD bool half_test_pass(float pw, float q2) { return !(pw < 0.0f && q2 < 0.0f); }
+
 struct CullBound {
     float cx, cy, cz, R;
 };

@@ -48,7 +48,26 @@ static float ref_disc(const float o[3], const float d[3], const float c[3], floa
 // disc of that sphere is >= 0 (or NaN), the block test must pass
 // (line_test_q, and for flat blocks also line_test_q_flat, on the bound
 // against thr * kCullThrScale, or thr' * kCullThrScaleSy for the stretched ray).
-static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
+// The reference's acceptance of sphere c (hit_world32's roots, best = +inf).
+static bool ref_accepts(const float o[3], const float d[3], const float c[3], float negr2, float a, float t_min) {
+    const float ocx = o[0] - c[0], ocy = o[1] - c[1], ocz = o[2] - c[2];
+    const float hb = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
+    const float disc = ref_disc(o, d, c, negr2, a);
+    if (disc < 0.0f) return false;
+    const float inv_a = 1.0f / a, sq = std::sqrt(disc);
+    const float rn = (-hb - sq) * inv_a;
+    if (!(rn < t_min || INFINITY < rn)) return true;
+    const float rf = (-hb + sq) * inv_a;
+    return !(rf < t_min || INFINITY < rf);
+}
+
+// Half-space part (rtx_prefilter.h HalfTest): whenever the reference accepts
+// the sphere (a root >= t_min, t_min 0 or 1e-3), the bound must pass both
+// tests. A fifth of the rays start on (or just inside or outside) the sphere,
+// half of those leaving it straight away from the bound's centre (the tight
+// case of the half test: the hit is at t ~ 0, the bound behind the origin).
+static void block_cases(long n, long &ref_pos, long &missed, double &max_used, long &acc_pos, long &half_missed,
+                        long &half_culled, double &half_max_used) {
     for (long k = 0; k < n; ++k) {
         double cd[3], dir[3], e[3], t[3];
         unit(cd);
@@ -102,6 +121,30 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
             o[i] = (float)(c[i] + dist * e[i] - along * dir[i]);
             d[i] = (float)(dlen * dir[i]);
         }
+        if (uni() < 0.2) {  // the origin on the sphere
+            double nv[3];
+            const bool tight = uni() < 0.5 && al > 0.0;
+            if (tight) {
+                for (int i = 0; i < 3; ++i) nv[i] = away[i] / al;
+            } else {
+                unit(nv);
+            }
+            const double delta = uni() < 0.7 ? std::pow(10.0, -9.0 + 7.0 * uni()) * (uni() < 0.5 ? -1.0 : 1.0)
+                                             : -uni();
+            double dv[3];
+            if (tight) {
+                double pt[3];
+                unit(pt);
+                const double tilt = uni() < 0.5 ? 0.0 : std::pow(10.0, -6.0 + 5.0 * uni());
+                for (int i = 0; i < 3; ++i) dv[i] = nv[i] + tilt * pt[i];
+            } else {
+                unit(dv);
+            }
+            for (int i = 0; i < 3; ++i) {
+                o[i] = (float)(c[i] + rr * (1.0 + delta) * nv[i]);
+                d[i] = (float)(dlen * dv[i]);
+            }
+        }
         const float r2 = c[3] * c[3];
         const float a = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
         double sm = 0.0;
@@ -132,6 +175,29 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used) {
             // the line's estimated dperp_b^2 against the bound's inflated R_b - thr_b
             const double used = ((double)b.R - q) / ((double)b.R - thr_b);
             if (used > max_used) max_used = used;
+        }
+        // the half test, in the bound's space (stretched for flat blocks), both op orders for flat
+        const float t_min = uni() < 0.5 ? 0.0f : 1e-3f;
+        const rtx::HalfTest H = flat ? rtx::half_test_setup(o[0], sy * o[1], o[2], d[0], d1s, d[2], as, thr_b, t_min)
+                                     : rtx::half_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, thr_b, t_min);
+        const float pw = rtx::half_test_pw(H, b.cx, b.cy, b.cz);
+        bool hp = rtx::half_test_pass(pw, rtx::half_test_q2(H, pw, b.R));
+        if (flat) {
+            const float pwf = rtx::half_test_pw_flat(H, rtx::half_test_kw(H, b.cy), b.cx, b.cz);
+            hp = hp && rtx::half_test_pass(pwf, rtx::half_test_q2(H, pwf, b.R));
+        }
+        const bool acc = ref_accepts(o, d, c, -r2, a, t_min);
+        acc_pos += acc;
+        half_culled += ref && !acc && !hp;
+        if (acc && !hp) {
+            if (++half_missed <= 5)
+                std::fprintf(stderr, "HALF MISS c=(%.9g %.9g %.9g) r=%.9g o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) pw=%.9g "
+                             "flat=%d\n", c[0], c[1], c[2], c[3], o[0], o[1], o[2], d[0], d[1], d[2], pw, (int)flat);
+        }
+        if (acc && pw < 0.0f && H.tha != INFINITY) {
+            // pw^2 against K = R_b a - 2 thr_b a: the geometric part is 1 / (1 + k) of it
+            const double used = (double)pw * pw / ((double)b.R * H.a + (double)H.tha);
+            if (used > half_max_used) half_max_used = used;
         }
     }
 }
@@ -215,12 +281,15 @@ int main(int argc, char **argv) {
             if (used > max_used) max_used = used;
         }
     }
-    long b_ref = 0, b_missed = 0;
-    double b_used = -1e300;
-    block_cases(n / 2, b_ref, b_missed, b_used);
+    long b_ref = 0, b_missed = 0, h_acc = 0, h_missed = 0, h_culled = 0;
+    double b_used = -1e300, h_used = -1e300;
+    block_cases(n / 2, b_ref, b_missed, b_used, h_acc, h_missed, h_culled, h_used);
     std::printf("{\"cases\": %ld, \"reference_candidates\": %ld, \"flagged\": %ld, \"false_positives\": %ld, "
                 "\"unsafe_lanes\": %ld, \"missed\": %ld, \"max_margin_used\": %.6g, \"block_cases\": %ld, "
-                "\"block_reference_candidates\": %ld, \"block_missed\": %ld, \"block_max_used\": %.9g}\n",
-                n, ref_pos, flagged, false_pos, unsafe, missed, max_used, n / 2, b_ref, b_missed, b_used);
-    return missed || b_missed ? 1 : 0;
+                "\"block_reference_candidates\": %ld, \"block_missed\": %ld, \"block_max_used\": %.9g, "
+                "\"block_reference_accepted\": %ld, \"half_missed\": %ld, \"half_culled\": %ld, "
+                "\"half_max_used\": %.9g}\n",
+                n, ref_pos, flagged, false_pos, unsafe, missed, max_used, n / 2, b_ref, b_missed, b_used, h_acc,
+                h_missed, h_culled, h_used);
+    return missed || b_missed || h_missed ? 1 : 0;
 }

@@ -8,7 +8,7 @@ prefilter flags every sphere whose reference fp32 discriminant is >= 0 (or
 NaN). tests/prefilter_check.cpp evaluates both, with the header's own code,
 on adversarial near-tangent cases and must find no miss; likewise for the
 culled scan's block bounds (a block is skipped only if no lane's line passes
-its bound). The GPU side of the same claims is
+its bound, or its bound is wholly behind every lane's origin). The GPU side of the same claims is
 test_gpu_parity.py::test_hit_world_grazing_rays (both scans).
 """
 import json
@@ -33,3 +33,10 @@ def test_prefilter_never_drops_a_reference_candidate(tmp_path):
     # of R_b, 1 / (1 + k) = 0.97 of it, never the rounding margins
     assert rep["block_missed"] == 0 and rep["block_reference_candidates"] > 500_000, rep
     assert rep["block_max_used"] < 0.98, rep
+    # the half-space part (rtx_prefilter.h HalfTest): no sphere the reference
+    # accepts (a root >= t_min) is behind a failed half test; the rays that
+    # leave a sphere straight away from its bound reach 1 / (1 + k) of K, and
+    # the test does cull reference candidates whose roots are behind
+    assert rep["half_missed"] == 0 and rep["block_reference_accepted"] > 300_000, rep
+    assert 0.9 < rep["half_max_used"] < 0.98, rep
+    assert rep["half_culled"] > 100_000, rep
