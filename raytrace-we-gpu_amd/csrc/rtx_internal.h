@@ -70,6 +70,9 @@ constexpr uint32_t kCullAlign = RTX_CULL_LEVELS >= 3 ? 512u : 64u;
 #ifndef RTX_CULL_HALF  // culled scan: a bound wholly behind the origin fails too (rtx_prefilter.h HalfTest)
 #define RTX_CULL_HALF 1
 #endif
+#ifndef RTX_CULL_HALF_SPHERES  // 1: also drop a flagged sphere wholly behind it (measured slower: R9s)
+#define RTX_CULL_HALF_SPHERES 0
+#endif
 #ifndef RTX_CULL_BFS  // the one-ray culled coop walks the levels breadth first (0: each lane its subtree)
 #define RTX_CULL_BFS 1
 #endif

@@ -742,7 +742,8 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     const float thr_b = T.thr * kCullThrScale;
     const f2v hdx = {H.dx, H.dx}, hdy = {H.dy, H.dy}, hdz = {H.dz, H.dz}, hnod = {H.nod, H.nod};
     const f2v ha = {H.a, H.a}, htha = {H.tha, H.tha};
-    const float kws1 = half_test_kw(Hs, kCullSy * S.flat_cy);
+    const float kws1 = half_test_kw(Hs, kCullSy * S.flat_cy), kwf1 = half_test_kw(H, S.flat_cy);
+    const f2v kwf = {kwf1, kwf1};
     const f2v kws = {kws1, kws1}, has = {Hs.a, Hs.a}, hthas = {Hs.tha, Hs.tha};
     // Q of the 4 pairs of an AoSoA-8 block of spheres or bounds (blk(i): its i-th float)
     auto quad = [&](auto flat, auto blk, f2v *q) {
@@ -786,7 +787,28 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
                 inv = (inv << 1) | (__float_as_uint(sq.y) >> 31);
                 inv = (inv << 1) | (__float_as_uint(sq.x) >> 31);
             }
-            const uint32_t mask = ~inv & 0xffu;
+            // the flagged spheres wholly behind the lane's origin drop out
+            // (the half test per sphere; only for blocks some lane flags)
+            uint32_t hm = 0xffu;
+            if (RTX_CULL_HALF_SPHERES) {
+                hm = 0u;
+#pragma unroll
+                for (int p = 3; p >= 0; --p) {
+                    const f2v cx = {v[2 * p], v[2 * p + 1]}, cz = {v[16 + 2 * p], v[17 + 2 * p]};
+                    const f2v R = {v[24 + 2 * p], v[25 + 2 * p]};
+                    f2v pw;
+                    if constexpr (decltype(flat)::value) {
+                        pw = fma2(cx, hdx, fma2(cz, hdz, kwf));
+                    } else {
+                        const f2v cy = {v[8 + 2 * p], v[9 + 2 * p]};
+                        pw = fma2(cx, hdx, fma2(cy, hdy, fma2(cz, hdz, hnod)));
+                    }
+                    const f2v q2 = fma2(-pw, pw, fma2(R, ha, htha));
+                    hm = (hm << 1) | (half_test_pass(pw.y, q2.y) ? 1u : 0u);
+                    hm = (hm << 1) | (half_test_pass(pw.x, q2.x) ? 1u : 0u);
+                }
+            }
+            const uint32_t mask = ~inv & hm & 0xffu;
             my[cnt * kRB] = (8u * bb) | (mask << 24);
             cnt += mask != 0u ? 1u : 0u;
             return __ballot(cnt == cand_of<true>()) != 0ull;
@@ -1360,7 +1382,10 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
             };
             auto test_sphere = [&](uint32_t pos) {
                 const float *q = S.cpre + 32u * (pos >> 3) + (pos & 7u);
-                return !(line_test_q(T, q[0], q[8], q[16], q[24]) < T.thr);
+                if (line_test_q(T, q[0], q[8], q[16], q[24]) < T.thr) return false;
+                if (!RTX_CULL_HALF_SPHERES) return true;
+                const float pw = half_test_pw(H, q[0], q[8], q[16]);
+                return half_test_pass(pw, half_test_q2(H, pw, q[24]));
             };
             // the child this lane takes: of the (lane >> 3)-th set bit of the
             // uniform mask m (the next 8 set bits are consumed)
@@ -1426,7 +1451,7 @@ __device__ __forceinline__ int hit_world_groups_culled(const KScene &S, uint64_t
                 while (mb != 0u) {
                     const uint32_t bb = 8u * gi + (uint32_t)__builtin_ctz(mb);
                     mb &= mb - 1u;
-                    uint32_t ms = block_mask(S.cpre + 32u * bb, T, T.thr);
+                    uint32_t ms = block_mask(S.cpre + 32u * bb, T, T.thr, RTX_CULL_HALF_SPHERES ? &H : nullptr);
 #pragma unroll 1
                     while (ms != 0u) {
                         const uint32_t pos = 8u * bb + (uint32_t)__builtin_ctz(ms);

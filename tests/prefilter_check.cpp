@@ -205,7 +205,8 @@ static void block_cases(long n, long &ref_pos, long &missed, double &max_used, l
 int main(int argc, char **argv) {
     const long n = argc > 1 ? std::atol(argv[1]) : 2000000;
     long ref_pos = 0, flagged = 0, missed = 0, unsafe = 0, false_pos = 0;
-    double max_used = -1e300;
+    long s_acc = 0, s_half_missed = 0, s_half_culled = 0;
+    double max_used = -1e300, s_half_used = -1e300;
     for (long k = 0; k < n; ++k) {
         double cd[3], dir[3], e[3];
         unit(cd);
@@ -250,6 +251,24 @@ int main(int argc, char **argv) {
             o[i] = (float)(cs * cd[i] + dist * e[i] - along * dir[i]);
             d[i] = (float)(dlen * dir[i]);
         }
+        if (uni() < 0.2) {  // the origin on (or just inside or outside) the sphere, a third leaving it radially
+            double nv[3], dv[3];
+            unit(nv);
+            const double delta = uni() < 0.7 ? std::pow(10.0, -9.0 + 7.0 * uni()) * (uni() < 0.5 ? -1.0 : 1.0)
+                                             : -uni();
+            if (uni() < 0.33) {
+                double pt[3];
+                unit(pt);
+                const double tilt = uni() < 0.5 ? 0.0 : std::pow(10.0, -6.0 + 5.0 * uni());
+                for (int i = 0; i < 3; ++i) dv[i] = nv[i] + tilt * pt[i];
+            } else {
+                unit(dv);
+            }
+            for (int i = 0; i < 3; ++i) {
+                o[i] = (float)(cs * cd[i] + r * (1.0 + delta) * nv[i]);
+                d[i] = (float)(dlen * dv[i]);
+            }
+        }
         const float rf = (float)r;
         const float r2 = rf * rf;
         const float a = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
@@ -280,6 +299,25 @@ int main(int argc, char **argv) {
             const double used = (((double)R - std::fmin(q, qf)) - r2) / ((double)R - T.thr - r2);
             if (used > max_used) max_used = used;
         }
+        // the sphere-level half test of the culled scan (the bounds' H: thr * kCullThrScale), both orders
+        const float t_min = uni() < 0.5 ? 0.0f : 1e-3f;
+        const rtx::HalfTest H =
+            rtx::half_test_setup(o[0], o[1], o[2], d[0], d[1], d[2], a, T.thr * rtx::kCullThrScale, t_min);
+        const float pw = rtx::half_test_pw(H, c[0], c[1], c[2]);
+        const float pwf = rtx::half_test_pw_flat(H, rtx::half_test_kw(H, c[1]), c[0], c[2]);
+        const bool hp = rtx::half_test_pass(pw, rtx::half_test_q2(H, pw, R)) &&
+                        rtx::half_test_pass(pwf, rtx::half_test_q2(H, pwf, R));
+        const bool acc = ref_accepts(o, d, c, -r2, a, t_min);
+        s_acc += acc;
+        s_half_culled += ref && !acc && !hp;
+        if (acc && !hp && ++s_half_missed <= 5)
+            std::fprintf(stderr, "SPHERE HALF MISS c=(%.9g %.9g %.9g) r=%.9g o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) "
+                         "pw=%.9g\n", c[0], c[1], c[2], rf, o[0], o[1], o[2], d[0], d[1], d[2], pw);
+        if (acc && std::fmin(pw, pwf) < 0.0f && H.tha != INFINITY) {
+            const double pm = std::fmin(pw, pwf);
+            const double used = pm * pm / ((double)R * H.a + (double)H.tha);
+            if (used > s_half_used) s_half_used = used;
+        }
     }
     long b_ref = 0, b_missed = 0, h_acc = 0, h_missed = 0, h_culled = 0;
     double b_used = -1e300, h_used = -1e300;
@@ -288,8 +326,9 @@ int main(int argc, char **argv) {
                 "\"unsafe_lanes\": %ld, \"missed\": %ld, \"max_margin_used\": %.6g, \"block_cases\": %ld, "
                 "\"block_reference_candidates\": %ld, \"block_missed\": %ld, \"block_max_used\": %.9g, "
                 "\"block_reference_accepted\": %ld, \"half_missed\": %ld, \"half_culled\": %ld, "
-                "\"half_max_used\": %.9g}\n",
+                "\"half_max_used\": %.9g, \"sphere_reference_accepted\": %ld, \"sphere_half_missed\": %ld, "
+                "\"sphere_half_culled\": %ld, \"sphere_half_max_used\": %.9g}\n",
                 n, ref_pos, flagged, false_pos, unsafe, missed, max_used, n / 2, b_ref, b_missed, b_used, h_acc,
-                h_missed, h_culled, h_used);
-    return missed || b_missed || h_missed ? 1 : 0;
+                h_missed, h_culled, h_used, s_acc, s_half_missed, s_half_culled, s_half_used);
+    return missed || b_missed || h_missed || s_half_missed ? 1 : 0;
 }

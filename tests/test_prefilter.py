@@ -40,3 +40,7 @@ def test_prefilter_never_drops_a_reference_candidate(tmp_path):
     assert rep["half_missed"] == 0 and rep["block_reference_accepted"] > 300_000, rep
     assert 0.9 < rep["half_max_used"] < 0.98, rep
     assert rep["half_culled"] > 100_000, rep
+    # the same test per sphere (RTX_CULL_HALF_SPHERES, an option: measured
+    # slower), on the single-sphere cases, a fifth of them starting on the sphere
+    assert rep["sphere_half_missed"] == 0 and rep["sphere_reference_accepted"] > 500_000, rep
+    assert rep["sphere_half_max_used"] < 1.0 and rep["sphere_half_culled"] > 100_000, rep
