@@ -255,6 +255,9 @@ RTX_HD bool half_test_pass(float pw, float q2) { return !(pw < 0.0f && q2 < 0.0f
 struct CullBound {
     float cx, cy, cz, R;
 };
+#ifndef RTX_CULL_CENTRE_ITERS  // centre search steps of cull_bound (0: the box centre)
+#define RTX_CULL_CENTRE_ITERS 64
+#endif
 // Spheres (cx, cy, cz, r)[m] as uploaded; flat: every centre has height
 // flat_cy (the bound's centre takes it exactly, so the 5-op test applies).
 // sy: the stretch along y (1, or kCullSy for a flat bound: then the centre
@@ -271,6 +274,36 @@ inline CullBound cull_bound(const float *const *sph, int m, bool flat, float fla
     b.cy = flat ? sy * flat_cy : (float)(sy * 0.5 * (lo[1] + hi[1]));
     b.cz = (float)(0.5 * (lo[2] + hi[2]));
     const double u = 5.9604644775390625e-08;
+#if RTX_CULL_CENTRE_ITERS > 0
+    {
+        // A tighter centre than the box's (the proof holds for any centre:
+        // rho is measured from the one chosen): Badoiu-Clarkson steps towards
+        // the farthest sphere surface, keeping the best; a flat bound's centre
+        // keeps its height (the 5-op test's per-ray cy term).
+        double c[3] = {b.cx, b.cy, b.cz}, best[3] = {c[0], c[1], c[2]}, best_rho = INFINITY;
+        for (int it = 1; it <= RTX_CULL_CENTRE_ITERS; ++it) {
+            double far = -1.0, fv[3] = {0, 0, 0};
+            for (int i = 0; i < m; ++i) {
+                const double v[3] = {sph[i][0] - c[0], sy * (double)sph[i][1] - c[1], sph[i][2] - c[2]};
+                const double dd = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                const double e = dd + sy * (double)sph[i][3];
+                if (e > far) {
+                    far = e;
+                    const double k = dd > 0.0 ? e / dd : 0.0;
+                    fv[0] = v[0] * k, fv[1] = v[1] * k, fv[2] = v[2] * k;
+                }
+            }
+            if (far < best_rho) best_rho = far, best[0] = c[0], best[1] = c[1], best[2] = c[2];
+            const double step = 1.0 / (it + 1);
+            c[0] += fv[0] * step;
+            if (!flat) c[1] += fv[1] * step;
+            c[2] += fv[2] * step;
+        }
+        b.cx = (float)best[0];
+        b.cy = flat ? b.cy : (float)best[1];
+        b.cz = (float)best[2];
+    }
+#endif
     double rho = 0.0;
     for (int i = 0; i < m; ++i) {
         const double dx = (double)sph[i][0] - b.cx, dy = (double)sy * sph[i][1] - b.cy, dz = (double)sph[i][2] - b.cz;
