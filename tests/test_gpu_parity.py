@@ -224,6 +224,48 @@ def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
     assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
 
 
+def surface_rays(sph, count, rng):
+    """Rays starting on (or within 1e-7..1e-2 of) a sphere's surface: half
+    leaving it radially (the tight case of the culled scan's half test: the
+    hit at t ~ 0, the sphere's bounds behind the origin), half in random
+    directions; direction lengths 1e-2..1e2."""
+    idx = rng.integers(0, len(sph), count)
+    c, r = sph[idx, :3].astype(np.float64), sph[idx, 3:4].astype(np.float64)
+    nrm = rng.normal(size=(count, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    delta = np.where(rng.random((count, 1)) < 0.3, 0.0,
+                     10.0 ** rng.uniform(-7, -2, (count, 1)) * rng.choice([-1.0, 1.0], (count, 1)))
+    o = c + r * (1.0 + delta) * nrm
+    radial = rng.random((count, 1)) < 0.5
+    d = np.where(radial, nrm + 1e-4 * rng.normal(size=(count, 3)) * (rng.random((count, 1)) < 0.5),
+                 rng.normal(size=(count, 3)))
+    d *= 10.0 ** rng.uniform(-2, 2, (count, 1))
+    return np.concatenate([o, d], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("mode", ["lane", "coop1", "coop8"])
+def test_hit_world_culled_half_test(gpu_ctx, oracle, rtx, mode):
+    """The culled scan's half test (a bound wholly behind the origin fails;
+    rtx_prefilter.h HalfTest) at its tight case — rays leaving a sphere's
+    surface, whose reference roots sit at t ~ 0 — at t_min 1e-6, 1e-3 and
+    0.5 (the API takes t_min > 0; the kernel's guard for t_min < 0 is
+    covered by tests/prefilter_check.cpp's t_min 0 cases), lane mode and the
+    coop (one ray per wave: breadth first; eight: the per-lane walk), bit for
+    bit against the oracle."""
+    rng = np.random.default_rng({"lane": 7, "coop1": 8, "coop8": 9}[mode])
+    world = rtx.random_world(25, depth=1, spp=1)
+    layer = world.spheres[:, 1] == np.float32(0.2)
+    world.spheres[layer, 3] = rng.uniform(0.05, 0.6, layer.sum()).astype(np.float32)
+    gpu_ctx.upload_world(world)
+    rays = np.concatenate([surface_rays(world.spheres, 5000, rng), grazing_rays(world.spheres, 1000, rng)])
+    start = {"lane": rtx.DEBUG_CULLED, "coop1": rtx.DEBUG_CULLED_COOP(1), "coop8": rtx.DEBUG_CULLED_COOP(8)}[mode]
+    for t_min in (1e-6, 0.001, 0.5):
+        want = oracle.hit_world_f32(world, rays, t_min)
+        got = gpu_ctx.debug_hit_world(rays, t_min=t_min, start_block=start)
+        assert_bits_equal(got, want, f"culled half test, {mode}, t_min={t_min}")
+        assert (want[:, 9] >= 0).mean() > 0.3
+
+
 @pytest.mark.parametrize("layout", ["all_flat", "no_flat"])
 def test_hit_world_culled_scan_sections(gpu_ctx, oracle, rtx, layout):
     """The culled layout's edge cases: a scene that is one flat layer but for
