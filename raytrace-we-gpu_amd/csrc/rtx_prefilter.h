@@ -191,17 +191,19 @@ constexpr double kCullK = 1.0 / 32.0;
 // |c_i - C_b| measured in the stretched space, sqrt(A_i) and sqrt(B) scaled
 // by s, and |o| <= |o'|: rho' = max_i (|A c_i - C'_b| + s sqrt(A_i)),
 // thr'_b = -(kPreMarginO + (1 + 1/k) 26u s^2) |o'|^2 - kPreFloor, which is
-// >= thr' * kCullThrScaleSy (1.6e-5 + 33 * 26u * 16 = 8.34e-4 <= 1.6e-5 * 53).
+// >= thr' * kCullThrScaleSy (s = 8: 1.6e-5 + 33 * 26u * 64 = 3.289e-3 <= 1.6e-5 * 206).
 // The layer's bounds become nearly spheres (the layer is ~0.4 thick, a
 // block 2 x 4 cells wide), and a line passing above a patch no longer passes
-// its bound: at C5 a wave's lines pass 2.0 % of the flat block bounds instead
-// of 4.6 % (tools/block_cull_sim.py on the sampled rays).
+// its bound: at C5 (s = 4) a wave's lines pass 2.0 % of the flat block bounds
+// instead of 4.6 % (tools/block_cull_sim.py on the sampled rays). s = 8 since
+// the half test (below): C5 138.7 -> 129.5 ms (2 and 16
+// slower; 4 was best without it).
 #ifndef RTX_CULL_SY  // the stretch (a power of two: the scaling is exact)
-#define RTX_CULL_SY 4
+#define RTX_CULL_SY 8
 #endif
 constexpr float kCullSy = (float)RTX_CULL_SY;
 static_assert(RTX_CULL_SY >= 1 && (RTX_CULL_SY & (RTX_CULL_SY - 1)) == 0, "the stretch is a power of two");
-// 1 + (1 + 1/k) 26u sy^2 / kPreMarginO, rounded up (53 at sy = 4)
+// 1 + (1 + 1/k) 26u sy^2 / kPreMarginO, rounded up (206 at sy = 8, 53 at 4)
 constexpr float kCullThrScaleSy =
     (float)(int)(2.0 + (1.0 + 1.0 / kCullK) * 26.0 * 5.9604644775390625e-08 * RTX_CULL_SY * RTX_CULL_SY / 1.6e-5);
 
@@ -221,8 +223,8 @@ constexpr float kCullThrScaleSy =
 // and pw_c^2 <= ((1+k) rho^2 + (1+1/k)(1.1 B + 11 e^2)) a whenever pw_c < 0;
 // K = fl(fma(R_b, a, fl(-2 thr_b a))) exceeds that: R_b holds (1+k) rho^2
 // (1 + 2e-6) and 1.6e-5 |C_b|^2, and -2 thr_b >= 2 (6.71e-5 |o|^2) covers
-// (1 + 1/k) 1.1 B = 5.6e-5 |o|^2 (stretched: 2 * 8.48e-4 |o'|^2 against
-// 33 * 1.1 * 16 * 26u = 9.0e-4 |o'|^2, the proof carrying over as for the
+// (1 + 1/k) 1.1 B = 5.6e-5 |o|^2 (stretched, s = 8: 2 * 3.30e-3 |o'|^2 against
+// 33 * 1.1 * 64 * 26u = 3.6e-3 |o'|^2, the proof carrying over as for the
 // line test: S p = S o + t S d is a point of the stretched ray). A bound
 // fails the half test iff pw_c < 0 and fl(fma(-pw_c, pw_c, K)) < 0; NaN
 // passes; thr_b = -inf (a lane outside the safe range) and t_min < 0 make
