@@ -56,8 +56,9 @@ clean:
 # product path):
 #   stress - candidate lists of 1 entry and coop resolve rounds of one scan
 #            step, so every overflow, round and fallback path runs all the
-#            time, and a 100 ms promotion valve (the heartbeat keeps live
-#            launches going) (tests/test_gpu_parity.py)
+#            time, and a 20 ms promotion valve (the heartbeat keeps live
+#            launches going), and the kernarg layout check (RTX_CHECK_KERNARG)
+#            (tests/test_gpu_parity.py)
 #   prof   - per-section clock sums (tools/section_prof.py)
 #   ptime  - per-pixel start/end times (tools/pixel_timeline.py)
 #   cprof  - per-section clocks of tier-1 coop segments (tools/coop_prof.py)
@@ -65,7 +66,7 @@ clean:
 # Ad-hoc A/B builds for tools/variant_bench.py:
 #   make adhoc V=name VFLAGS="-DRTX_...=..."   -> lib/variants/librtx_name.so
 VARIANTS := stress prof ptime cprof rays
-VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=10000000ull
+VFLAGS_stress        := -DRTX_CAND=1 -DRTX_CAND_PF=1 -DRTX_GF_STEPS=1 -DRTX_PROM_VALVE_TICKS=2000000ull -DRTX_CHECK_KERNARG=1
 VFLAGS_prof          := -DRTX_DIAG_PROF=1
 VFLAGS_ptime         := -DRTX_DIAG_PIXEL=1
 VFLAGS_cprof         := -DRTX_DIAG_COOP=1
@@ -74,7 +75,7 @@ VDIR := $(LIBDIR)/variants
 
 variants: $(foreach v,$(VARIANTS),$(VDIR)/librtx_$(v).so)
 
-$(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS)
+$(VDIR)/librtx_%.so: $(SRC)/rtx_kernels.hip $(SRC)/rtx_api.hip $(SRC)/rtx_host.cpp $(HDRS) Makefile
 	mkdir -p $(VDIR)/$*
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c $(SRC)/rtx_kernels.hip -o $(VDIR)/$*/k.o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -DRTX_SRC_SHA='"$(SRC_SHA)"' -DRTX_VARIANT='"$*"' -c $(SRC)/rtx_api.hip -o $(VDIR)/$*/a.o

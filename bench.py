@@ -10,12 +10,24 @@ rank 0 de-interleaves into the image. Scene/camera are resident on the
 device before timing. Launch:
 
     python bench.py [--gpus 1] [--steps 10] [--warmup 2]
+    python bench.py --gpus N ...        (N > 1: launches its N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+`--gpus N` outside torch.distributed.run (WORLD_SIZE unset) starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child
+process and exits with its code; the parent makes no GPU call (it counts the
+visible devices in a child of its own). `--spawn` does the same for N = 1
+(the one-rank RCCL path).
+
 Rank 0 prints ONE JSON line. `value` = pixels*spp*steps / max-over-ranks
 wall time of the timed steps: the frame is split across ranks, so the work
-per step is fixed as N grows ("scaling": "strong").
+per step is fixed as N grows ("scaling": "strong"). An N > 1
+line also carries `dist` (the process group's backend and size as
+torch.distributed saw them, the RCCL version, each rank's device and its
+per-step render / gather / de-interleave times from HIP events on the
+step's stream) and `parity` (rows of the gathered frame, two from every
+rank's share, bit for bit against the fp32 oracle after timing).
 """
 from __future__ import annotations
 
@@ -62,6 +74,9 @@ def parse():
     p.add_argument("--gather", action="store_true",
                    help="N=1: run the N-rank path anyway (process group over RCCL, row tiles, one gather, "
                         "de-interleave): a one-GPU rehearsal of it")
+    p.add_argument("--spawn", action="store_true",
+                   help="launch the ranks through torch.distributed.run as a child process even for N=1 "
+                        "(N>1 outside torch.distributed.run always does)")
     p.add_argument("--dump-image", default="", help=argparse.SUPPRESS)  # rank 0 saves the last frame (.npy)
     p.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--probe-parts", type=int, default=0, help=argparse.SUPPRESS)  # --probe: an R-way split
@@ -472,11 +487,109 @@ def build_provenance(rtx):
             "arch": info.get("arch")}
 
 
+# ---------------------------------------------------------------------------
+# Rank launcher: `bench.py --gpus N` outside torch.distributed.run
+# ---------------------------------------------------------------------------
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_command(n: int, script: str, script_args, port: int, python: str = sys.executable):
+    """The child command that runs `script` as n ranks of one node:
+    torch.distributed.run, rendezvous on 127.0.0.1 (the container hostname
+    may not resolve)."""
+    return [python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", script] + list(script_args)
+
+
+def rank_launch_env(base=None) -> dict:
+    """The ranks' environment: the caller's, with dmabuf IPC kept (the host
+    driver supports only that; RCCL fails without it) and a marker so a rank
+    never launches again."""
+    env = dict(os.environ if base is None else base)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    env["RTX_BENCH_RANKS_LAUNCHED"] = "1"
+    return env
+
+
+def visible_gpus(timeout: float = 300.0) -> int:
+    """HIP devices visible to a fresh process, counted in a child so this one
+    never touches the GPU (it is about to start the ranks)."""
+    code = "import torch; print(torch.cuda.device_count())"
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return 0
+
+
+def launch_ranks(n: int, script: str, script_args, timeout=None) -> int:
+    """Run `script` as n ranks (torch.distributed.run in a child process) and
+    return its exit code; the ranks' stdout and stderr are this process's."""
+    cmd = rank_launch_command(n, script, script_args, free_port())
+    try:
+        return subprocess.run(cmd, env=rank_launch_env(), timeout=timeout).returncode
+    except subprocess.TimeoutExpired:
+        return 124
+
+
+def spawn_main(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1, or --spawn) outside torch.distributed.run:
+    start the N ranks as a fresh child and exit with its code. Fewer than N
+    visible devices is an error, not a smaller run."""
+    n = max(1, args.gpus)
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible HIP devices, found {have} "
+              f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', 'unset')})", file=sys.stderr)
+        return 3
+    rest = [a for a in argv if a != "--spawn"]
+    if n == 1 and "--gather" not in rest:
+        rest.append("--gather")  # one rank still runs the process group and the RCCL gather
+    return launch_ranks(n, os.path.abspath(__file__), rest)
+
+
+def parity_rows(H, T, R, per_part=2):
+    """`per_part` rows from every rank's share of an R-way row-tile split
+    (its first row, then evenly spaced), ascending."""
+    import numpy as np
+    import rtx
+    rows = []
+    for p in range(R):
+        ids = rtx.part_row_ids(H, T, p, R)
+        rows += [int(ids[int(k)]) for k in np.linspace(0, len(ids) - 1, per_part + 1)[:-1]]
+    return sorted(set(rows))
+
+
+def gathered_parity(world, frame, image, H, T, R, per_part=2):
+    """Rows of the gathered frame against the fp32 oracle (bit for bit):
+    `per_part` rows from every rank's share, so every rank's rows and the
+    de-interleave are checked."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    rows = parity_rows(H, T, R, per_part)
+    threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16))
+    want, _ = oracle.render_rows(world, frame, np.array(rows, np.uint32), nthreads=threads)
+    got = image[rows]
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    return {"rows": rows, "rows_checked": len(rows), "ranks_covered": R, "values_differing": int((~same).sum()),
+            "bit_exact": bool(same.all()), "checker": "fp32 oracle (oracle/rtx_oracle.c), after timing"}
+
+
 def main():
     args = parse()
     if args.probe:
         probe(args)
         return
+    if "WORLD_SIZE" not in os.environ and not os.environ.get("RTX_BENCH_RANKS_LAUNCHED") \
+            and (args.gpus > 1 or args.spawn):
+        sys.exit(spawn_main(args, sys.argv[1:]))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -487,7 +600,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         if world_size == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+            raise SystemExit("--gpus N>1: WORLD_SIZE is 1 in a launched rank")
         args.gpus = world_size
     torch.cuda.set_device(local_rank)
     collective = world_size > 1 or args.gather
@@ -521,6 +634,19 @@ def main():
                          render_part=lambda send, part, nparts: ctx.render_rows(T, part, nparts, send.data_ptr()),
                          deinterleave=lambda g, img: ctx.deinterleave(g.data_ptr(), W, H, T, R, img.data_ptr()))
         image = fg.image
+        # per-step phase times of this rank: HIP events on the step's stream
+        # (the gather's completion is ordered on it: torch waits the RCCL
+        # stream into the current one), recorded in the timed steps only
+        phase_events, recording = [], [False]
+
+        def mark(name):
+            if recording[0]:
+                if name == "start":
+                    phase_events.append({})
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                phase_events[-1][name] = ev
+        fg.mark = mark
 
         def step():
             fg.step()
@@ -535,17 +661,47 @@ def main():
     barrier()
     ctx.stats_reset()
     barrier()
+    if collective:
+        recording[0] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if collective:
+        recording[0] = False
     barrier()
+    elapsed_local = elapsed
     if collective:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = ctx.stats()
+    dist_info = None
+    if collective:
+        def phase_ms(a, b):
+            v = [e[a].elapsed_time(e[b]) for e in phase_events if a in e and b in e]
+            return round(sum(v) / len(v), 4) if v else None
+        props = torch.cuda.get_device_properties(local_rank)
+        mine = {"rank": rank, "local_rank": local_rank, "device": props.name,
+                "pci_bus_id": getattr(props, "pci_bus_id", None), "rows": fg.rows,
+                "render_ms": phase_ms("start", "rendered"), "gather_ms": phase_ms("rendered", "gathered"),
+                "deinterleave_ms": phase_ms("gathered", "done"), "step_ms": phase_ms("start", "done"),
+                "wall_ms_per_step": round(elapsed_local / args.steps * 1e3, 4),
+                "kernel_ms": round(st.kernel_ms / max(1, st.launches), 4),
+                "segments_per_launch": int(st.segments // max(1, st.launches))}
+        per_rank = [None] * world_size
+        dist.all_gather_object(per_rank, mine)
+        nccl_v = torch.cuda.nccl.version() if hasattr(torch.cuda, "nccl") else None
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "rccl_version": ".".join(str(x) for x in nccl_v) if isinstance(nccl_v, tuple) else nccl_v,
+                     "launcher": "bench.py self-launch (torch.distributed.run child)"
+                                 if os.environ.get("RTX_BENCH_RANKS_LAUNCHED") else
+                                 ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "direct"),
+                     "per_rank": per_rank,
+                     "note": "render = rtx_render_rows into the rank's send buffer; gather = one RCCL gather to "
+                             "rank 0 (torch.distributed 'nccl'); deinterleave = rtx_deinterleave_rows on rank 0; "
+                             "each the mean over the timed steps of HIP events on the step's stream"}
     if args.dump_image and rank == 0:
         np.save(args.dump_image, image.cpu().numpy())
 
@@ -564,10 +720,12 @@ def main():
             executed = pmc_valu(args, n_cu, launch_ms)
             if world.count <= 640 and args.rng == "chain":
                 ceiling = issue_ceiling(args, ctx, executed, n_cu)
-        host_img = image.cpu().numpy() if R == 1 else None
+        host_img = image.cpu().numpy()
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:
             cpu, parity = cpu_baseline(args, world, frame, host_img, args.cpu_seconds)
+        if collective and parity is None:  # the gathered frame: rows of every rank's share
+            parity = gathered_parity(world, frame, host_img, H, T, R)
         # the 1/2/4/8-GPU split rehearsed on this device (BASELINE.json metric:
         # "1/2/4/8-GPU scaling"); the real N-GPU runs are the driver's
         parts = None
@@ -643,6 +801,7 @@ def main():
                              else round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                              "measured_kind": "rocprofv3 PMC traffic per launch / launch time"},
             "part_scaling": parts,
+            "dist": dist_info,
             "cpu_baseline": cpu,
             "parity": parity,
             "per_sample_rng": per_sample,

@@ -38,8 +38,11 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 142 /* 1.4.2 */
+#define RTX_VERSION 143 /* 1.4.3 */
 /* ABI notes.
+ *  1.4.3: RTX_DEBUG_CULLED_COOP_LANE(q) (the culled coop's per-lane walk);
+ *         RTX_ERR_INCOMPLETE's message names which promotion wait fired and
+ *         what the server saw (no layout change).
  *  1.4.2: rtx_debug_hit_world_from's start_block RTX_DEBUG_CULLED and
  *         RTX_DEBUG_CULLED_COOP(q) (the culled scan, lane mode and group
  *         coop; no layout change).
@@ -410,6 +413,10 @@ RTX_API int rtx_debug_hit_world(rtx_ctx *ctx, const float *rays, uint32_t nrays,
  * the culled scan split over a wave's lanes as the render's frame tail and
  * heavy tiers run it, q rays per wave (64 / 2^ceil(log2 q) lanes per ray). */
 #define RTX_DEBUG_CULLED_COOP(q) (0xFFFFFF00u | (unsigned)(q))
+/* start_block = RTX_DEBUG_CULLED_COOP_LANE(q): the same split with each lane
+ * walking its own subtree (the per-sample kernel's form; RTX_DEBUG_CULLED_COOP
+ * walks one ray's levels breadth first). */
+#define RTX_DEBUG_CULLED_COOP_LANE(q) (0xFFFFFE00u | (unsigned)(q))
 RTX_API int rtx_debug_hit_world_from(rtx_ctx *ctx, const float *rays, uint32_t nrays,
                                      float t_min, float t_max, uint32_t start_block,
                                      float *out);

@@ -51,9 +51,12 @@ constexpr size_t kEventRing = 64;  // initial ring size
 
 // Device counter words (unsigned long long): [0] ray segments, [2] pixel-queue
 // head (low half), [3] rtx_debug_pixel_cost's segments, [4] launch error bits
-// (rtx::kErr*, low half; read back and cleared by check_errors), [1], [5] spare.
-constexpr size_t kCounterWords = 6;
+// (rtx::kErr*, low half; read back and cleared by check_errors), [1], [5] spare,
+// [6, 6 + kErrDiagWords) the first promotion-valve firing's record
+// (KParams::err_diag, rtx_internal.h).
 constexpr size_t kErrWord = 4;
+constexpr size_t kErrDiag = 6;
+constexpr size_t kCounterWords = kErrDiag + rtx::kErrDiagWords;
 
 }  // namespace
 
@@ -128,15 +131,42 @@ int set_device(rtx_ctx *c) {
 // check set (KParams::errors), reported once and cleared. A set bit means a
 // launch left pixels unwritten (rtx_kernels.hip take_promoted).
 int check_errors(rtx_ctx *c, const char *what) {
-    unsigned long long bits = 0;
-    RTX_HIP(hipMemcpyAsync(&bits, c->d_counters + kErrWord, sizeof(bits), hipMemcpyDeviceToHost, c->stream));
+    unsigned long long w[kCounterWords - kErrWord];  // the error word, [5], the valve record
+    RTX_HIP(hipMemcpyAsync(w, c->d_counters + kErrWord, sizeof(w), hipMemcpyDeviceToHost, c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
+    const unsigned long long bits = w[0];
     if (bits == 0) return RTX_OK;
-    RTX_HIP(hipMemsetAsync(c->d_counters + kErrWord, 0, sizeof(bits), c->stream));
+    RTX_HIP(hipMemsetAsync(c->d_counters + kErrWord, 0, sizeof(w), c->stream));
     RTX_HIP(hipStreamSynchronize(c->stream));
+    const double valve_ms = (double)rtx::kPromValveTicks * 1e-5;  // s_memrealtime: 100 MHz
+    char buf[160];
     std::string why;
-    if (bits & rtx::kErrPromTimeout) why += " promotion service saw no progress for 10 s and left;";
+    if (bits & rtx::kErrPromTimeout) {
+        std::snprintf(buf, sizeof buf, " a promotion server polled for %.0f ms seeing no pixel written and no "
+                      "heartbeat, and left;", valve_ms);
+        why += buf;
+    }
+    if (bits & rtx::kErrPromEntryWait) {
+        std::snprintf(buf, sizeof buf, " a claimed promotion entry was not published within %.0f ms;", valve_ms);
+        why += buf;
+    }
     if (bits & rtx::kErrPromTorn) why += " a promotion entry was out of range;";
+    if (bits & rtx::kErrKernarg) why += " a kernel's argument segment did not begin with its KParams (check build);";
+    const unsigned long long *d = w + (kErrDiag - kErrWord);
+    if (d[0] != 0) {
+        auto lo = [](unsigned long long v) { return (unsigned)(v & 0xffffffffull); };
+        auto hi = [](unsigned long long v) { return (unsigned)(v >> 32); };
+        std::snprintf(buf, sizeof buf, " first firing: bit %u by %s, %.3f ms since progress, last heartbeat "
+                      "%.3f ms before;", lo(d[0]) & 0xffu, (lo(d[0]) >> 8) == 2u ? "k_trace" : "k_render",
+                      (double)d[1] * 1e-5, (double)lo(d[2]) * 1.024e-2);
+        why += buf;
+        std::snprintf(buf, sizeof buf, " queue claimed %u taken %u, written %u of %u (npix %u, k_render "
+                      "started %u);", lo(d[3]), hi(d[3]), lo(d[4]), hi(d[4]), hi(d[5]), lo(d[5]));
+        why += buf;
+        std::snprintf(buf, sizeof buf, " polls %u, observer stalls %u, longest poll gap %.3f ms, entry %d",
+                      lo(d[6]), hi(d[6]), (double)lo(d[7]) * 1e-5, (int)hi(d[7]));
+        why += buf;
+    }
     return fail(RTX_ERR_INCOMPLETE, std::string(what) + ": a render launch left pixels unwritten:" + why);
 }
 
@@ -793,6 +823,7 @@ static rtx::KParams make_params(const rtx_ctx *c, uint32_t rows, uint32_t tile_r
     p.counters = c->d_counters;
     p.queue = reinterpret_cast<uint32_t *>(c->d_counters + 2);
     p.errors = reinterpret_cast<uint32_t *>(c->d_counters + kErrWord);
+    p.err_diag = c->d_counters + kErrDiag;
     p.depth = c->depth;
     p.spp = c->spp;
     p.width = f.width;
@@ -1139,6 +1170,8 @@ int rtx_debug_scan_rate(rtx_ctx *c, uint32_t reps, float *ms, unsigned long long
     if (rc) return rc;
     const rtx_frame &f = c->frame;
     rtx::KParams p = make_params(c, f.height, 1, 0, 1, nullptr, nullptr, 0, f.frame_index);
+    if (!rtx::debug_scan_rate_supported(p))  // refused before any HIP call: every HIP error below is hip_fail's
+        return fail(RTX_ERR_INVALID, "rtx_debug_scan_rate: scenes up to 640 spheres and a non-empty frame only");
     unsigned long long *sink = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     uint32_t waves = 0;
@@ -1154,7 +1187,6 @@ int rtx_debug_scan_rate(rtx_ctx *c, uint32_t reps, float *ms, unsigned long long
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(sink);
-    if (e == hipErrorInvalidValue) return fail(RTX_ERR_INVALID, "rtx_debug_scan_rate: scenes up to 640 spheres");
     if (e != hipSuccess) return hip_fail(e, "rtx_debug_scan_rate");
     *wave_segments = (unsigned long long)waves * reps;
     return RTX_OK;

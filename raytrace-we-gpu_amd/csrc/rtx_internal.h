@@ -86,14 +86,34 @@ constexpr uint32_t kPad = 8;  // spheres per AoSoA block
 constexpr uint32_t kFrameLambertGuard = 1u;  // = RTX_FRAME_LAMBERT_GUARD
 
 // KParams::errors bits: a launch that sets one left pixels unwritten.
-constexpr uint32_t kErrPromTimeout = 1u;  // a promotion server saw no progress for kPromValveTicks and left
-constexpr uint32_t kErrPromTorn = 2u;     // a promotion entry held an out-of-range pixel or sample
+constexpr uint32_t kErrPromTimeout = 1u;    // a promotion server saw no progress for kPromValveTicks and left
+constexpr uint32_t kErrPromTorn = 2u;       // a promotion entry held an out-of-range pixel or sample
+constexpr uint32_t kErrPromEntryWait = 4u;  // a claimed promotion entry was not published within kPromValveTicks
+constexpr uint32_t kErrKernarg = 8u;        // check build: a kernel's kernarg segment did not begin with its KParams
+
+// The promotion valve (rtx_kernels.hip take_promoted): a server that has
+// been polling for this long with no pixel written and no heartbeat leaves
+// and flags the launch. s_memrealtime ticks (100 MHz). The stress build
+// (Makefile) sets its own.
+#ifndef RTX_PROM_VALVE_TICKS
+#define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s
+#endif
+constexpr unsigned long long kPromValveTicks = RTX_PROM_VALVE_TICKS;
+// KParams::err_diag: what the first server whose valve fired saw, kErrDiagWords
+// u64 words (rtx_api.hip check_errors prints them):
+//   [0] error bit | who << 8 (1 k_render server, 2 k_trace helper)
+//   [1] ticks since the server last saw progress   [2] heartbeat age, s_memrealtime >> 10 units
+//   [3] prom[0] | prom[1] << 32 (entries claimed, taken)   [4] prom[2] | target << 32 (written, to write)
+//   [5] prom[3] | npix << 32   [6] polls since progress | observer stalls << 32
+//   [7] longest poll gap (ticks) | entry index waited on << 32 (~0: none)
+constexpr uint32_t kErrDiagWords = 8;
 
 // Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
 struct KParams {
     KScene scene;
     float4 *out;                   // part's rows, contiguous, row-major
     float4 *out_slot;              // cost-ordered render: the image by queue slot (k_unpermute), or NULL
+    uint32_t stage_tag;            // ... the launch's tag in a staged pixel's w (k_unpermute moves only those)
     unsigned long long *counters;  // [0] += ray segments (hit_world calls)
     uint32_t *queue;               // pixel queue head (zeroed before each launch)
     uint32_t depth, spp;
@@ -129,6 +149,7 @@ struct KParams {
                                    // [3] k_render has started (set by its workgroup 0)
                                    // [4] heartbeat: s_memrealtime >> 10 of a tracing wave (valve); NULL: off
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
+    unsigned long long *err_diag;  // kErrDiagWords: the first valve firing's record (NULL: none)
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0
@@ -213,7 +234,9 @@ hipError_t launch_deinterleave(const float4 *gathered, float4 *image, uint32_t w
 hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t nrays,
                                   float t_min, float t_max, uint32_t start_block, float *out,
                                   hipStream_t stream);
-// hit_world alone at the render's occupancy (rtx_debug_scan_rate); *waves: the grid's waves
+// hit_world alone at the render's occupancy (rtx_debug_scan_rate); *waves: the grid's waves.
+// Scenes that fit the coop's LDS copy (the C2 kernels), non-empty frames only:
+bool debug_scan_rate_supported(const KParams &p);
 hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
                                   hipStream_t stream);
 hipError_t launch_debug_math(int fn, const float *in0, const float *in1, uint32_t n,

@@ -1556,10 +1556,12 @@ __device__ __forceinline__ void output_pixel(const KParams &P, uint32_t gid, f3 
     o.y = to_gamma(sum.y / n);
     o.z = to_gamma(sum.z / n);
     o.w = 1.0f;
-    if (P.out_slot && slot != ~0u)
+    if (P.out_slot && slot != ~0u) {
+        o.w = __uint_as_float(P.stage_tag);  // this launch's staged pixel (k_unpermute writes w = 1)
         P.out_slot[slot] = o;
-    else
+    } else {
         P.out[gid] = o;
+    }
 }
 
 #ifndef RTX_EXTRA_BYTES
@@ -1842,7 +1844,28 @@ __device__ __forceinline__ void count_segments(const KParams &P, uint32_t segs) 
     if ((threadIdx.x & 63u) == 0u && segs != 0u) atomicAdd(P.counters, (unsigned long long)segs);
 }
 
-__device__ __forceinline__ Frame load_frame(const KParams &) { return Frame{}; }  // (frame_vals)
+// The kernel's frame token (start_sample reads the constants through
+// frame_vals). frame_vals assumes the kernarg segment begins with the
+// kernel's KParams; the check build (RTX_CHECK_KERNARG, on in the stress
+// build the GPU tests run) compares what it reads there with `P` — the
+// kernel's own argument at every call site — and flags the launch
+// (kErrKernarg: rtx_sync / rtx_get_stats report it) if a kernel ever breaks
+// that layout.
+#ifndef RTX_CHECK_KERNARG
+#define RTX_CHECK_KERNARG 0
+#endif
+__device__ __forceinline__ Frame load_frame(const KParams &P) {
+    if constexpr (RTX_CHECK_KERNARG != 0) {
+        const FrameVals v = frame_vals();
+        const bool same = __float_as_uint(v.img_w) == __float_as_uint(P.img_w) &&
+                          __float_as_uint(v.img_h) == __float_as_uint(P.img_h) &&
+                          __float_as_uint(v.org.x) == __float_as_uint(P.org[0]) &&
+                          __float_as_uint(v.llc.z) == __float_as_uint(P.llc[2]) &&
+                          __float_as_uint(v.lens_r) == __float_as_uint(P.lens_r);
+        if (!same && P.errors && (threadIdx.x & 63u) == 0u) atomicOr(P.errors, kErrKernarg);
+    }
+    return Frame{};
+}
 
 // Start pixel `gid` (local index of this launch's rows) on this lane.
 // Launches with spp == 0 or depth == 0 never get here (k_render_trivial).
@@ -2181,16 +2204,68 @@ __device__ __forceinline__ void regroup(Lane &W, uint32_t lg, uint32_t nlg, uint
 // but live chain — a big scene, a high spp — never trips the valve however
 // long it runs without another pixel finishing; only a launch in
 // which nothing traces any more does. The stress build (make all) runs with
-// a 100 ms valve (a beat every 6.25 ms), so its GPU tests exercise exactly
+// a 20 ms valve (a beat every 1.25 ms), so its GPU tests exercise exactly
 // that.
-#ifndef RTX_PROM_VALVE_TICKS
-#define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s of s_memrealtime (100 MHz)
-#endif
-constexpr unsigned long long kPromValveTicks = RTX_PROM_VALVE_TICKS;
+// The valve's clock runs only while the server itself runs (Valve): a poll
+// that comes more than a beat period after the server's previous one means
+// the server was not running either (its wave descheduled, the queue
+// preempted), which is no evidence that nothing else ran, so the clock
+// restarts there. A server that keeps polling on time with nothing written
+// and no heartbeat still leaves after kPromValveTicks. The wait for a claimed
+// entry's epoch has its own clock from the claim and its own bit
+// (kErrPromEntryWait). The first firing leaves its record in KParams::err_diag.
+// (kPromValveTicks: rtx_internal.h)
 constexpr unsigned long long kBeatTicks = kPromValveTicks / 16u;
 constexpr uint32_t kBeatShift = 10;  // prom[4] holds s_memrealtime >> 10 (10.24 us units, wraps every ~12 h)
 __device__ __forceinline__ void flag_error(const KParams &P, uint32_t bit) {
     if (P.errors && (threadIdx.x & 63u) == 0u) atomicOr(P.errors, bit);
+}
+struct Valve {
+    unsigned long long t0, last, max_gap;
+    uint32_t polls, stalls;
+    __device__ __forceinline__ void start() {
+        t0 = last = __builtin_amdgcn_s_memrealtime();
+        max_gap = 0ull;
+        polls = stalls = 0u;
+    }
+    __device__ __forceinline__ void progress() {  // a pixel written or a heartbeat seen
+        t0 = last;
+        max_gap = 0ull;
+        polls = 0u;
+    }
+    // one poll; true once the server has polled on time for kPromValveTicks
+    // since it last saw progress
+    __device__ __forceinline__ bool expired() {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long gap = now - last;
+        last = now;
+        ++polls;
+        if (gap > kBeatTicks) {  // the server itself did not run: restart the clock
+            t0 = now;
+            ++stalls;
+        } else if (gap > max_gap) {
+            max_gap = gap;
+        }
+        return now - t0 > kPromValveTicks;
+    }
+};
+// The valve fired: flag the launch and, if no server has yet, record what
+// this one saw (rtx_internal.h kErrDiagWords). Wave-uniform call.
+__device__ __noinline__ void valve_fire(const KParams &P, uint32_t bit, uint32_t who, const Valve &V, uint32_t target,
+                                        uint32_t npix, uint32_t entry) {
+    flag_error(P, bit);
+    if (P.err_diag == nullptr || (threadIdx.x & 63u) != 0u) return;
+    if (atomicCAS(P.err_diag, 0ull, (unsigned long long)(bit | who << 8)) != 0ull) return;
+    auto ld = [](const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    unsigned long long *d = P.err_diag;
+    d[1] = now - V.t0;
+    d[2] = (uint32_t)((uint32_t)(now >> kBeatShift) - ld(&P.prom[4]));
+    d[3] = ld(&P.prom[0]) | (unsigned long long)ld(&P.prom[1]) << 32;
+    d[4] = ld(&P.prom[2]) | (unsigned long long)target << 32;
+    d[5] = ld(&P.prom[3]) | (unsigned long long)npix << 32;
+    d[6] = V.polls | (unsigned long long)V.stalls << 32;
+    d[7] = (uint32_t)min(V.max_gap, 0xffffffffull) | (unsigned long long)entry << 32;
 }
 // The heartbeat (wave-uniform; `last` is the wave's previous beat).
 __device__ __forceinline__ void beat(const KParams &P, unsigned long long &last) {
@@ -2203,7 +2278,8 @@ __device__ __forceinline__ void beat(const KParams &P, unsigned long long &last)
 }
 __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, uint32_t npix, uint32_t target,
                                               bool helper, Lane &W) {
-    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    Valve V;
+    V.start();
     uint32_t seen = ~0u;
     __builtin_amdgcn_s_setprio(0);
     auto ld = [](const uint32_t *p) {
@@ -2218,7 +2294,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         if (done != seen || bt != seen_beat) {  // progress (a pixel written, or a heartbeat): the valve restarts
             seen = done;
             seen_beat = bt;
-            t0 = __builtin_amdgcn_s_memrealtime();
+            V.progress();
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         const uint32_t t = min(ld(&P.prom[0]), P.prom_cap);
@@ -2228,10 +2304,12 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
         if (got != ~0u) {
             const uint32_t *e = P.prom_q + 8u * got;
+            Valve E;  // the entry's producer publishes it right after claiming the slot: its own clock
+            E.start();
             while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
-                    flag_error(P, kErrPromTimeout);
+                if (E.expired()) {
+                    valve_fire(P, kErrPromEntryWait, 1u, E, target, npix, got);
                     return false;
                 }
             }
@@ -2255,8 +2333,8 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
             return true;
         }
         if (h >= t) __builtin_amdgcn_s_sleep(127);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
-            flag_error(P, kErrPromTimeout);
+        if (V.expired()) {
+            valve_fire(P, kErrPromTimeout, 1u, V, target, npix, ~0u);
             return false;
         }
     }
@@ -2492,7 +2570,8 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
     auto ld = [](const uint32_t *p) {
         return (uint32_t)__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     };
-    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    Valve V;
+    V.start();
     uint32_t seen = ~0u, seen_beat = 0;
     const uint32_t nneed = (uint32_t)__popcll(need);
     // this lane's group among the idle ones (only meaningful in idle groups)
@@ -2504,7 +2583,7 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
         if (done != seen || bt != seen_beat) {  // progress: a pixel written or a heartbeat
             seen = done;
             seen_beat = bt;
-            t0 = __builtin_amdgcn_s_memrealtime();
+            V.progress();
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         const uint32_t t = min(ld(&P.prom[0]), P.prom_cap);
@@ -2515,12 +2594,17 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
             if (lane == 0u) won = atomicCAS(&P.prom[1], h, h + want) == h ? 1u : 0u;
             won = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)won, 0, 64));
             if (won == 0u) continue;  // another server took them first
-            bool torn = false;
+            bool torn = false, late = false;
+            Valve E;  // each claimed entry's wait has its own clock from the claim (kErrPromEntryWait)
+            E.start();
             if (!W.active && rank < want) {
                 const uint32_t *e = P.prom_q + 8u * (h + rank);
                 while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) break;
+                    if (E.expired()) {
+                        late = true;
+                        break;
+                    }
                 }
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the fields are read after the epoch matched
                 W.gid = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2529,9 +2613,9 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
                 W.acc = mk3(__uint_as_float(__hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                             __uint_as_float(__hip_atomic_load(e + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                             __uint_as_float(__hip_atomic_load(e + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-                const bool late = __hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch;
-                torn = late || W.gid >= npix || W.sample >= P.spp;
-                if (!torn) {
+                late = late || __hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch;
+                torn = !late && (W.gid >= npix || W.sample >= P.spp);
+                if (!torn && !late) {
                     lane_pixel(P, W.gid, W.x, W.y);
                     W.seg0 = W.segs;
                     W.slot = ~0u;  // a promoted pixel: counted in prom[2] when written
@@ -2540,9 +2624,18 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
                     diag_pixel_start(P, W.gid, 3ull);
                 }
             }
-            if (__ballot(torn) != 0ull) {  // never: a late or torn entry ends the wave's service, not the GPU
-                flag_error(P, kErrPromTorn | kErrPromTimeout);
-                W.active = W.active && !torn;
+            // never: a late or torn entry ends the wave's service, not the GPU
+            const uint64_t lb = __ballot(late), tb = __ballot(torn);
+            if ((lb | tb) != 0ull) {
+                if (lb != 0ull) {
+                    const uint32_t src = (uint32_t)__builtin_ctzll(lb);  // the record: the first late lane's wait
+                    E.t0 = __shfl(E.t0, (int)src, 64);
+                    E.polls = (uint32_t)__shfl((int)E.polls, (int)src, 64);
+                    E.stalls = (uint32_t)__shfl((int)E.stalls, (int)src, 64);
+                    E.max_gap = __shfl(E.max_gap, (int)src, 64);
+                    valve_fire(P, kErrPromEntryWait, 2u, E, target, npix, h + (uint32_t)__shfl((int)rank, (int)src, 64));
+                }
+                if (tb != 0ull) flag_error(P, kErrPromTorn);
                 return -1;
             }
             return (int)want;
@@ -2550,8 +2643,8 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
         if (!blocking) return 0;
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_sleep(127);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kPromValveTicks) {
-            flag_error(P, kErrPromTimeout);
+        if (V.expired()) {
+            valve_fire(P, kErrPromTimeout, 2u, V, target, npix, ~0u);
             return -1;
         }
     }
@@ -3092,14 +3185,17 @@ __global__ void __launch_bounds__(kBlock) k_deinterleave(const float4 *__restric
 
 // The cost-ordered render's image, from its slot-ordered staging buffer to
 // the linear framebuffer (ShaderCompute.hlsl:314's one texel per pixel, in
-// pixel order): pixel i is stage[inv[i]], read gathered, stored coalesced; a
-// promoted pixel (stage w = 0) was written to out[i] by whoever finished it.
+// pixel order): pixel i is stage[inv[i]], read gathered, stored coalesced.
+// Only slots this launch staged are moved (w holds the launch's tag,
+// KParams::stage_tag): a promoted pixel (stage w = 0) was written to out[i] by
+// whoever finished it, and a slot a launch left unwritten (the valve fired:
+// RTX_ERR_INCOMPLETE) keeps out[i] as it was, never another frame's pixel.
 __global__ void __launch_bounds__(kBlock) k_unpermute(const float4 *__restrict__ stage, const uint32_t *__restrict__ inv,
-                                                      uint32_t npix, float4 *__restrict__ out) {
+                                                      uint32_t npix, uint32_t tag, float4 *__restrict__ out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= npix) return;
     const float4 v = stage[inv[i]];
-    if (v.w != 0.0f) out[i] = v;
+    if (__float_as_uint(v.w) == tag) out[i] = make_float4(v.x, v.y, v.z, 1.0f);
 }
 
 // One hit record of rtx_debug_hit_world (include/rtx.h): hit, t, p, normal,
@@ -3153,8 +3249,12 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
 // (hit_world_groups_culled, the large-scene tail / heavy tiers) with q rays
 // per wave, i.e. 64 / 2^ceil(log2 q) lanes per ray (q > 32: two chunks of
 // 32 rays at 2 lanes each); a ray whose group met a non-finite root takes
-// the in-order path, as in the render.
+// the in-order path, as in the render. kDebugCulledCoopLane | q: the same
+// with the per-lane walk (hit_world_groups_culled<false>: k_render_ps's
+// form, whose one-ray case q = 1 the breadth-first selector never runs).
 constexpr uint32_t kDebugCulledCoop = 0xffffff00u;
+constexpr uint32_t kDebugCulledCoopLane = 0xfffffe00u;
+template <bool kBfs>
 __global__ void __launch_bounds__(kRB) k_debug_hit_world_coop(const KScene S, const float *rays, uint32_t nrays,
                                                               float t_min, float t_max, uint32_t q, float *out) {
     __shared__ uint32_t list[list_bytes<true>() / sizeof(uint32_t)];
@@ -3171,8 +3271,8 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world_coop(const KScene S, co
     const float inv_a = 1.0f / a;
     float best = t_max;
     bool seq = false;
-    int idx = hit_world_groups_culled(S, __ballot(active), active, o, d, a, inv_a, t_min,
-                                      ws_all + w * (kCoopWaveBytes / 4), best, seq);
+    int idx = hit_world_groups_culled<kBfs>(S, __ballot(active), active, o, d, a, inv_a, t_min,
+                                            ws_all + w * (kCoopWaveBytes / 4), best, seq);
     if (!active) return;
     if (seq) {
         best = t_max;
@@ -3470,6 +3570,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     q.cost_spp = c.spp;
     q.perm = sched.perm;
     q.out_slot = sched.stage;  // the image in queue-slot order, k_unpermute after the render
+    q.stage_tag = sched.epoch;  // nonzero, new every launch: the staged pixels' w
     q.state = sched.state;
     q.prio_slots = (uint32_t)((double)blocks * kRB * tune.prio_frac);
     q.heavy = heavy;
@@ -3533,7 +3634,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     if (e == hipSuccess && trace_waves > 0) e = hipStreamWaitEvent(stream, sched.ev_join, 0);
     if (e == hipSuccess && sched.stage) {
         hipLaunchKernelGGL(k_unpermute, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, sched.stage, sched.inv,
-                           (uint32_t)lanes, p.out);
+                           (uint32_t)lanes, q.stage_tag, p.out);
         e = hipGetLastError();
     }
     return e;
@@ -3553,10 +3654,15 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
                                   float t_max, uint32_t start_block, float *out, hipStream_t stream) {
     if (nrays == 0) return hipSuccess;
     const uint32_t q = start_block & 0xffu;
-    if ((start_block & ~0xffu) == kDebugCulledCoop && q >= 1u && q <= 64u && s.cpre) {
+    const uint32_t sel = start_block & ~0xffu;
+    if ((sel == kDebugCulledCoop || sel == kDebugCulledCoopLane) && q >= 1u && q <= 64u && s.cpre) {
         const uint32_t waves = ceil_div(nrays, q);
-        hipLaunchKernelGGL(k_debug_hit_world_coop, dim3(ceil_div(waves, kRB / 64u)), dim3(kRB), 0, stream, s, rays,
-                           nrays, t_min, t_max, q, out);
+        if (sel == kDebugCulledCoop)
+            hipLaunchKernelGGL(k_debug_hit_world_coop<true>, dim3(ceil_div(waves, kRB / 64u)), dim3(kRB), 0, stream, s,
+                               rays, nrays, t_min, t_max, q, out);
+        else
+            hipLaunchKernelGGL(k_debug_hit_world_coop<false>, dim3(ceil_div(waves, kRB / 64u)), dim3(kRB), 0, stream,
+                               s, rays, nrays, t_min, t_max, q, out);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
@@ -3564,9 +3670,13 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
     return hipGetLastError();
 }
 
+bool debug_scan_rate_supported(const KParams &p) {
+    return p.scene.n <= kCoopLds && !use_pf(p.scene) && (uint64_t)p.rows_local * p.width != 0;
+}
+
 hipError_t launch_debug_scan_rate(const KParams &p, uint32_t reps, unsigned long long *sink, uint32_t *waves,
                                   hipStream_t stream) {
-    if (p.scene.n > kCoopLds || use_pf(p.scene) || (uint64_t)p.rows_local * p.width == 0) return hipErrorInvalidValue;
+    if (!debug_scan_rate_supported(p)) return hipErrorInvalidValue;
     const size_t lds = kListBytes + kCoopBytes + (size_t)coop_lds_bytes(p.scene.n);
     const uint32_t blocks = resident_blocks((const void *)k_debug_scan_rate, lds);
     *waves = blocks * (kRB / 64);

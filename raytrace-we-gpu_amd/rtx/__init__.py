@@ -36,6 +36,14 @@ def DEBUG_CULLED_COOP(q: int) -> int:
     if not 1 <= q <= 64:
         raise ValueError("q must be in 1..64")
     return 0xFFFFFF00 | q
+
+
+def DEBUG_CULLED_COOP_LANE(q: int) -> int:
+    """rtx_debug_hit_world_from: the culled group coop with the per-lane walk
+    (the per-sample kernel's form), q rays per wave (RTX_DEBUG_CULLED_COOP_LANE)."""
+    if not 1 <= q <= 64:
+        raise ValueError("q must be in 1..64")
+    return 0xFFFFFE00 | q
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
@@ -362,7 +370,7 @@ class Context:
 
     def render_rows(self, tile_rows: int, part: int, nparts: int, d_out: Optional[int] = None):
         _check(self._lib.rtx_render_rows(self._h, tile_rows, part, nparts,
-                                         C.c_void_p(d_out or 0)), "rtx_render_rows")
+                                         C.c_void_p(d_out or 0)), "rtx_render_rows", self._lib)
 
     def render(self):
         _check(self._lib.rtx_render(self._h), "rtx_render", self._lib)
@@ -376,7 +384,7 @@ class Context:
                      d_image: int):
         _check(self._lib.rtx_deinterleave_rows(self._h, C.c_void_p(d_gathered), width, height,
                                                tile_rows, nparts, C.c_void_p(d_image)),
-               "rtx_deinterleave_rows")
+               "rtx_deinterleave_rows", self._lib)
 
     def sync(self):
         _check(self._lib.rtx_sync(self._h), "rtx_sync", self._lib)
@@ -471,7 +479,7 @@ class Context:
         out = np.zeros(3 * a.size, np.float32)
         _check(self._lib.rtx_debug_math(self._h, FN[fn], _fptr(a),
                                         _fptr(b) if b is not None else None, a.size, _fptr(out)),
-               "rtx_debug_math")
+               "rtx_debug_math", self._lib)
         return out.reshape(a.size, 3) if FN[fn] >= FN["hash1"] else out[:a.size]
 
     def debug_lambert_dir(self, p: np.ndarray, nrm: np.ndarray, rius: np.ndarray, guard: bool) -> np.ndarray:
@@ -483,7 +491,7 @@ class Context:
         out = np.zeros_like(a)
         fn = FN["lambert_dir_guard" if guard else "lambert_dir"]
         _check(self._lib.rtx_debug_math(self._h, fn, _fptr(a), _fptr(b), a.shape[0], _fptr(out)),
-               "rtx_debug_math")
+               "rtx_debug_math", self._lib)
         return out
 
 
@@ -494,24 +502,24 @@ class DeviceArray:
         self.ctx, self.shape, self.dtype = ctx, tuple(shape), np.dtype(dtype)
         self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
         p = C.c_void_p()
-        _check(ctx._lib.rtx_alloc(ctx._h, self.nbytes, C.byref(p)), "rtx_alloc")
+        _check(ctx._lib.rtx_alloc(ctx._h, self.nbytes, C.byref(p)), "rtx_alloc", ctx._lib)
         self.ptr = int(p.value)
 
     def numpy(self) -> np.ndarray:
         out = np.empty(self.shape, self.dtype)
         _check(self.ctx._lib.rtx_copy_to_host(self.ctx._h, out.ctypes.data, C.c_void_p(self.ptr),
-                                              self.nbytes), "rtx_copy_to_host")
+                                              self.nbytes), "rtx_copy_to_host", self.ctx._lib)
         return out
 
     def upload(self, a: np.ndarray):
         a = np.ascontiguousarray(a, self.dtype)
         assert a.nbytes == self.nbytes
         _check(self.ctx._lib.rtx_copy_to_device(self.ctx._h, C.c_void_p(self.ptr), a.ctypes.data,
-                                                self.nbytes), "rtx_copy_to_device")
+                                                self.nbytes), "rtx_copy_to_device", self.ctx._lib)
 
     def free(self):
         if self.ptr and self.ctx._h:
-            _check(self.ctx._lib.rtx_free(self.ctx._h, C.c_void_p(self.ptr)), "rtx_free")
+            _check(self.ctx._lib.rtx_free(self.ctx._h, C.c_void_p(self.ptr)), "rtx_free", self.ctx._lib)
         self.ptr = 0
 
     def __del__(self):

@@ -62,20 +62,31 @@ class FrameGather:
         # one-GPU rehearsal of the N-rank path: RCCL's gather on the render's
         # buffers, the same stream order)
         self.collective = collective or world_size > 1
+        # optional phase marks: mark("start" | "rendered" | "gathered" | "done")
+        # at the step's phase boundaries (bench.py records HIP events there)
+        self.mark: Optional[Callable] = None
+
+    def _mark(self, name):
+        if self.mark is not None:
+            self.mark(name)
 
     def step(self):
         import torch.distributed as dist
+        self._mark("start")
         self.render_part(self.send, self.rank, self.R)
+        self._mark("rendered")
         if self.collective:
             gl = list(self.gathered.unbind(0)) if self.rank == self.root else None
             dist.gather(self.send, gather_list=gl, dst=self.root)
         elif self.rank == self.root:
             self.gathered[0].copy_(self.send)
+        self._mark("gathered")
         if self.rank == self.root:
             if self.deinterleave is not None:
                 self.deinterleave(self.gathered, self.image)
             else:
                 self.image.copy_(self._deinterleave_torch())
+        self._mark("done")
         return self.image
 
     def _deinterleave_torch(self):

@@ -125,3 +125,40 @@ def test_bench_rccl_path_one_rank(tmp_path, oracle, rtx):
     rows = np.linspace(1, H - 2, 8).astype(np.uint32)
     want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
     np.testing.assert_array_equal(got[rows].view(np.uint32), want.view(np.uint32))
+
+
+def test_bench_spawn_one_rank(tmp_path, oracle, rtx):
+    """`bench.py --gpus 1 --spawn`: the self-launch the driver's `--gpus N`
+    run takes — bench.py starts torch.distributed.run as a
+    child, the rank runs the RCCL path — and the N-rank line's schema: the
+    process group as torch.distributed saw it, the RCCL version, the rank's
+    device and per-step render / gather / de-interleave times, and the
+    gathered frame's rows bit-exact against the oracle."""
+    import json
+    import subprocess
+    W, H, spp = 320, 180, 16
+    img_path = str(tmp_path / "img.npy")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--spawn", "--width", str(W),
+           "--height", str(H), "--spp", str(spp), "--steps", "3", "--warmup", "1", "--pmc", "off",
+           "--cpu-seconds", "0", "--parts", "", "--per-sample", "0", "--dump-image", img_path]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["config"]["parallelism"] == "row-tiles x1 + RCCL gather"
+    d = line["dist"]
+    assert d["backend"] == "nccl" and d["world_size"] == 1 and d["rccl_version"]
+    assert d["launcher"].startswith("bench.py self-launch")
+    (pr,) = d["per_rank"]
+    assert pr["rank"] == 0 and pr["rows"] == H
+    for k in ("render_ms", "gather_ms", "deinterleave_ms", "step_ms"):
+        assert pr[k] is not None and pr[k] >= 0, k
+    assert pr["render_ms"] <= pr["step_ms"]
+    p = line["parity"]
+    assert p["bit_exact"] and p["rows_checked"] == 2 and p["values_differing"] == 0
+    got = np.load(img_path)
+    world = rtx.random_world(11, depth=50, spp=spp)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    rows = np.linspace(1, H - 2, 8).astype(np.uint32)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(got[rows].view(np.uint32), want.view(np.uint32))

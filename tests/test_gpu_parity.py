@@ -193,21 +193,25 @@ def test_hit_world_grazing_rays(gpu_ctx, oracle, rtx, scan):
     assert (want[:, 0] == 1).mean() > 0.3
 
 
+@pytest.mark.parametrize("walk", ["bfs", "lane"])
 @pytest.mark.parametrize("q", [1, 2, 5, 8, 17, 32, 64])
-def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
+def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q, walk):
     """The culled scan split over a wave's lanes (hit_world_groups_culled: the
     large-scene frame tail, heavy tiers and promoted pixels), q rays per wave
-    (64 lanes per ray at q = 1 down to 2 at q = 32; q > 32 in two chunks): grazing rays
+    (64 lanes per ray at q = 1 down to 2 at q = 32; q > 32 in two chunks), in
+    both walks: k_render's (one ray per wave breadth first) and the per-lane
+    walk k_render_ps runs at every q: grazing rays
     over a 2,504-sphere scene (its flat layer's radii 0.05..0.6), aimed and random rays over a scene of
     duplicated spheres (ties), bit for bit against the oracle."""
+    coop = rtx.DEBUG_CULLED_COOP if walk == "bfs" else rtx.DEBUG_CULLED_COOP_LANE
     rng = np.random.default_rng(100 + q)
     world = rtx.random_world(25, depth=1, spp=1)
     layer = world.spheres[:, 1] == np.float32(0.2)  # the flat layer, with radii 0.05..0.6 instead of 0.2
     world.spheres[layer, 3] = rng.uniform(0.05, 0.6, layer.sum()).astype(np.float32)
     rays = grazing_rays(world.spheres, 4000, rng, xaxis_frac=0.05)
     gpu_ctx.upload_world(world)
-    got = gpu_ctx.debug_hit_world(rays, start_block=rtx.DEBUG_CULLED_COOP(q))
-    assert_bits_equal(got, oracle.hit_world_f32(world, rays), f"culled coop q={q}, grazing")
+    got = gpu_ctx.debug_hit_world(rays, start_block=coop(q))
+    assert_bits_equal(got, oracle.hit_world_f32(world, rays), f"culled coop {walk} q={q}, grazing")
     base = np.concatenate([rng.uniform(-20, 20, (900, 1)), rng.uniform(0, 2, (900, 1)),
                            rng.uniform(-20, 20, (900, 1)), rng.uniform(0.2, 0.9, (900, 1))], 1)
     sph = np.concatenate([base, base[::-1]]).astype(np.float32)
@@ -218,8 +222,8 @@ def test_hit_world_culled_coop(gpu_ctx, oracle, rtx, q):
     d = (sph[rng.integers(0, n, 3000), :3] - o) + rng.normal(scale=0.1, size=(3000, 3))
     rays = np.concatenate([np.concatenate([o, d], 1), rng.normal(size=(1000, 6)) * 10]).astype(np.float32)
     want = oracle.hit_world_f32(dup, rays, 0.001)
-    got = gpu_ctx.debug_hit_world(rays, t_min=0.001, start_block=rtx.DEBUG_CULLED_COOP(q))
-    assert_bits_equal(got, want, f"culled coop q={q}, ties")
+    got = gpu_ctx.debug_hit_world(rays, t_min=0.001, start_block=coop(q))
+    assert_bits_equal(got, want, f"culled coop {walk} q={q}, ties")
     hit = want[:, 9] >= 0
     assert (want[hit, 9] >= n // 2).all(), "a tie must go to the later duplicate"
 
@@ -243,7 +247,7 @@ def surface_rays(sph, count, rng):
     return np.concatenate([o, d], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("mode", ["lane", "coop1", "coop8"])
+@pytest.mark.parametrize("mode", ["lane", "coop1", "coop8", "coop1_lane"])
 def test_hit_world_culled_half_test(gpu_ctx, oracle, rtx, mode):
     """The culled scan's half test (a bound wholly behind the origin fails;
     rtx_prefilter.h HalfTest) at its tight case — rays leaving a sphere's
@@ -252,13 +256,14 @@ def test_hit_world_culled_half_test(gpu_ctx, oracle, rtx, mode):
     covered by tests/prefilter_check.cpp's t_min 0 cases), lane mode and the
     coop (one ray per wave: breadth first; eight: the per-lane walk), bit for
     bit against the oracle."""
-    rng = np.random.default_rng({"lane": 7, "coop1": 8, "coop8": 9}[mode])
+    rng = np.random.default_rng({"lane": 7, "coop1": 8, "coop8": 9, "coop1_lane": 10}[mode])
     world = rtx.random_world(25, depth=1, spp=1)
     layer = world.spheres[:, 1] == np.float32(0.2)
     world.spheres[layer, 3] = rng.uniform(0.05, 0.6, layer.sum()).astype(np.float32)
     gpu_ctx.upload_world(world)
     rays = np.concatenate([surface_rays(world.spheres, 5000, rng), grazing_rays(world.spheres, 1000, rng)])
-    start = {"lane": rtx.DEBUG_CULLED, "coop1": rtx.DEBUG_CULLED_COOP(1), "coop8": rtx.DEBUG_CULLED_COOP(8)}[mode]
+    start = {"lane": rtx.DEBUG_CULLED, "coop1": rtx.DEBUG_CULLED_COOP(1), "coop8": rtx.DEBUG_CULLED_COOP(8),
+             "coop1_lane": rtx.DEBUG_CULLED_COOP_LANE(1)}[mode]
     for t_min in (1e-6, 0.001, 0.5):
         want = oracle.hit_world_f32(world, rays, t_min)
         got = gpu_ctx.debug_hit_world(rays, t_min=t_min, start_block=start)
@@ -286,7 +291,7 @@ def test_hit_world_culled_scan_sections(gpu_ctx, oracle, rtx, layout):
     rays = rays.astype(np.float32)
     want = oracle.hit_world_f32(world, rays)
     for start, what in ((rtx.DEBUG_CULLED, "lane"), (rtx.DEBUG_CULLED_COOP(1), "coop 1"),
-                        (rtx.DEBUG_CULLED_COOP(8), "coop 8")):
+                        (rtx.DEBUG_CULLED_COOP(8), "coop 8"), (rtx.DEBUG_CULLED_COOP_LANE(1), "coop 1, per-lane walk")):
         assert_bits_equal(gpu_ctx.debug_hit_world(rays, start_block=start), want, f"{layout}, {what}")
     assert (want[:, 0] == 1).mean() > 0.4
 
@@ -1044,12 +1049,13 @@ def test_promotion_across_the_chip(request, oracle, rtx, ctx_name):
     producers and servers sit on all 8). The launch must complete (no
     RTX_ERR_INCOMPLETE from rtx_get_stats), rows bit-exact, and the segment
     count equal to an independent exact-grid pass's. Through the stress build
-    the promotion valve is 100 ms: the launch completes only if
+    the promotion valve is 20 ms: the launch completes only if
     the tracing waves' heartbeat counts as progress while no pixel finishes
     (a 2 ms valve fired here in R7e while only full waves, which had not
     seen the queue exhausted and did not beat yet, were tracing; a 20 ms one
-    fired once in R8x, on a frame whose kernels had not changed: the stress
-    build's slowest stretches are longer than that)."""
+    fired once in R8x, profiles/R8x_gtest_valve_fire.log: since round 6 the
+    valve's clock runs only while the server itself runs, the entry wait has
+    its own clock and bit, and a firing reports what the server saw)."""
     gpu_ctx = request.getfixturevalue(ctx_name)
     W, H, T = 1280, 720, 5
     world = rtx.random_world(11, depth=50, spp=12)
