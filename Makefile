@@ -11,7 +11,7 @@ BINDIR    := $(PKG)/bin
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function
 LIB       := $(LIBDIR)/librtx.so
 CLI       := $(BINDIR)/rtx_cli
-HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)/rtx_prefilter.h
+HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)/rtx_prefilter.h $(SRC)/rtx_grid.h
 # Build provenance (rtx_build_info): the library records the hash of the
 # sources it was built from; bench.py compares it with the tree's
 # (tools/src_sha.py computes the same hash).

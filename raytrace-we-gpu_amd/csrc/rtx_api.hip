@@ -63,6 +63,9 @@ constexpr size_t kCounterWords = kErrDiag + rtx::kErrDiagWords;
 #ifndef RTX_FLAT
 #define RTX_FLAT 1
 #endif
+#ifndef RTX_GRID_UPLOAD  // A/B build: 0 = no layer grid (every block of the flat run is scanned)
+#define RTX_GRID_UPLOAD 1
+#endif
 
 struct rtx_ctx {
     int device = 0;
@@ -83,6 +86,9 @@ struct rtx_ctx {
     uint32_t *d_cperm = nullptr;
     float4 *d_ccen = nullptr;
     uint32_t n_cpad = 0, cflat_lo = 0;
+    // layer grid of the flat run (small scenes; rtx_grid.h; none: null):
+    // its LayerGrid, then the cells' block masks
+    rtx::LayerGrid *d_grid = nullptr;
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
@@ -152,20 +158,23 @@ int check_errors(rtx_ctx *c, const char *what) {
     }
     if (bits & rtx::kErrPromTorn) why += " a promotion entry was out of range;";
     if (bits & rtx::kErrKernarg) why += " a kernel's argument segment did not begin with its KParams (check build);";
-    const unsigned long long *d = w + (kErrDiag - kErrWord);
-    if (d[0] != 0) {
-        auto lo = [](unsigned long long v) { return (unsigned)(v & 0xffffffffull); };
-        auto hi = [](unsigned long long v) { return (unsigned)(v >> 32); };
-        std::snprintf(buf, sizeof buf, " first firing: bit %u by %s, %.3f ms since progress, last heartbeat "
-                      "%.3f ms before;", lo(d[0]) & 0xffu, (lo(d[0]) >> 8) == 2u ? "k_trace" : "k_render",
-                      (double)d[1] * 1e-5, (double)lo(d[2]) * 1.024e-2);
+    const unsigned long long d = w[kErrDiag - kErrWord];
+    if (d != 0) {
+        const unsigned lo = (unsigned)d, age = (unsigned)(d >> 32);
+        std::snprintf(buf, sizeof buf, " first firing: bit %u by a %s server, %.2f ms since it saw progress, the "
+                      "heartbeat %.2f ms old, %u stalls of the server itself;", lo & 0xfu,
+                      ((lo >> 4) & 0xfu) == 2u ? "k_trace" : "k_render", (double)(lo >> 16) * 1.024e-2,
+                      (double)age * 1.024e-2, (lo >> 8) & 0xffu);
         why += buf;
-        std::snprintf(buf, sizeof buf, " queue claimed %u taken %u, written %u of %u (npix %u, k_render "
-                      "started %u);", lo(d[3]), hi(d[3]), lo(d[4]), hi(d[4]), hi(d[5]), lo(d[5]));
-        why += buf;
-        std::snprintf(buf, sizeof buf, " polls %u, observer stalls %u, longest poll gap %.3f ms, entry %d",
-                      lo(d[6]), hi(d[6]), (double)lo(d[7]) * 1e-5, (int)hi(d[7]));
-        why += buf;
+        // the last launch's queue counters (zeroed at its start, still in memory)
+        uint32_t q[5] = {0, 0, 0, 0, 0};
+        if (c->d_sched && c->sched_pixels &&
+            hipMemcpy(q, c->d_sched + 2 * c->sched_pixels + 2 * rtx::kCostBuckets + 8, sizeof q,
+                      hipMemcpyDeviceToHost) == hipSuccess) {
+            std::snprintf(buf, sizeof buf, " last launch's queue: claimed %u, taken %u, k_render pixels written %u, "
+                          "k_render started %u", q[0], q[1], q[2], q[3]);
+            why += buf;
+        }
     }
     return fail(RTX_ERR_INCOMPLETE, std::string(what) + ": a render launch left pixels unwritten:" + why);
 }
@@ -183,6 +192,8 @@ void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_cbnd3);
     (void)hipFree(c->d_cperm);
     (void)hipFree(c->d_ccen);
+    (void)hipFree(c->d_grid);
+    c->d_grid = nullptr;
     c->d_cpre = c->d_cbnd = c->d_cbnd2 = c->d_cbnd3 = nullptr;
     c->d_cperm = nullptr;
     c->d_ccen = nullptr;
@@ -218,6 +229,7 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.ccen = c->d_ccen;
     s.n_cpad = c->n_cpad;
     s.cflat_lo = c->cflat_lo;
+    s.grid = c->d_grid;
     return s;
 }
 
@@ -692,6 +704,11 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     CullLayout cl;
     const bool cull = RTX_CULL && n_pad > rtx::kScanPfMin;  // the large-scene (kPF) kernels scan it
     if (cull) cl = build_cull(w, pre4, flat_hi > flat_lo, flat_cy);
+    // the small-scene lane-mode scan's layer grid over the flat run (rtx_grid.h)
+    rtx::LayerGrid grid{};
+    std::vector<unsigned long long> gcell;
+    const bool has_grid = RTX_GRID_UPLOAD && !cull && n_pad <= rtx::kScanPfMin && flat_hi > flat_lo &&
+                          rtx::build_layer_grid(w->spheres, 8 * flat_lo, std::min(8 * flat_hi, n), grid, gcell);
     RTX_HIP(hipStreamSynchronize(c->stream));
     free_world(c);
     const size_t cap = n ? n : 1;
@@ -733,6 +750,16 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         RTX_HIP(hipStreamSynchronize(c->stream));
         c->n_cpad = (uint32_t)cl.perm.size();
         c->cflat_lo = cl.flat_lo;
+    }
+    if (has_grid) {
+        static_assert(sizeof(rtx::LayerGrid) % 8 == 0, "the cells follow the LayerGrid, 8-byte aligned");
+        std::vector<unsigned long long> buf(sizeof(rtx::LayerGrid) / 8 + gcell.size());
+        std::memcpy(buf.data(), &grid, sizeof grid);
+        std::memcpy(buf.data() + sizeof(rtx::LayerGrid) / 8, gcell.data(), gcell.size() * sizeof(unsigned long long));
+        RTX_HIP(hipMalloc(&c->d_grid, buf.size() * sizeof(unsigned long long)));
+        RTX_HIP(hipMemcpyAsync(c->d_grid, buf.data(), buf.size() * sizeof(unsigned long long), hipMemcpyHostToDevice,
+                               c->stream));
+        RTX_HIP(hipStreamSynchronize(c->stream));
     }
     if (c->n != n) c->n_changed = true;
     c->n = n;

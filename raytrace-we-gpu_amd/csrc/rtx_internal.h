@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rtx_grid.h"
+
 namespace rtx {
 
 // Device scene layout (all in HBM, read-only):
@@ -56,6 +58,10 @@ struct KScene {
     const float4 *ccen;
     const uint32_t *cperm;
     uint32_t n_cpad, cflat_lo;
+    // layer grid of the flat run (small scenes; rtx_grid.h): its LayerGrid,
+    // then per cell the mask of the run's blocks it may need (NULL: none,
+    // every block is scanned)
+    const LayerGrid *grid;
 };
 
 #ifndef RTX_CULL  // A/B build: 0 = no culled layout (the large-scene lane-mode scan visits every block)
@@ -99,14 +105,13 @@ constexpr uint32_t kErrKernarg = 8u;        // check build: a kernel's kernarg s
 #define RTX_PROM_VALVE_TICKS 1000000000ull  // 10 s
 #endif
 constexpr unsigned long long kPromValveTicks = RTX_PROM_VALVE_TICKS;
-// KParams::err_diag: what the first server whose valve fired saw, kErrDiagWords
-// u64 words (rtx_api.hip check_errors prints them):
-//   [0] error bit | who << 8 (1 k_render server, 2 k_trace helper)
-//   [1] ticks since the server last saw progress   [2] heartbeat age, s_memrealtime >> 10 units
-//   [3] prom[0] | prom[1] << 32 (entries claimed, taken)   [4] prom[2] | target << 32 (written, to write)
-//   [5] prom[3] | npix << 32   [6] polls since progress | observer stalls << 32
-//   [7] longest poll gap (ticks) | entry index waited on << 32 (~0: none)
-constexpr uint32_t kErrDiagWords = 8;
+// KParams::err_diag: what the first server whose valve fired saw, one u64
+// (rtx_api.hip check_errors prints it with the launch's queue counters):
+//   bits 0-3 the error bit, 4-7 who (1 k_render server, 2 k_trace helper),
+//   8-15 the server's own stalls (polls more than a beat period apart),
+//   16-31 time since it last saw progress, 32-63 the heartbeat's age, both in
+//   s_memrealtime >> 10 units (10.24 us)
+constexpr uint32_t kErrDiagWords = 1;
 
 // Per-launch constants (~ cbuffer b0 PerFrame + sceneValues of b1).
 struct KParams {
@@ -149,7 +154,7 @@ struct KParams {
                                    // [3] k_render has started (set by its workgroup 0)
                                    // [4] heartbeat: s_memrealtime >> 10 of a tracing wave (valve); NULL: off
     uint32_t *errors;              // launch error bits (kErr*), read back by rtx_sync / rtx_get_stats
-    unsigned long long *err_diag;  // kErrDiagWords: the first valve firing's record (NULL: none)
+    unsigned long long *err_diag;  // the first valve firing's record (kErrDiagWords; NULL: none)
     uint32_t *prom_q;              // [prom_cap][8] (gid, sample, seed, acc.xyz, -, epoch)
     uint32_t prom_cap, prom_min, epoch;
     uint32_t *heavy;               // [0] tier-1 counter [1] kh [2] tier-2 counter [3] k1 [4] k0

@@ -371,7 +371,8 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base) {
 template <bool kPF, bool kFlat, bool kTile = false>
 __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_t end, const LineTest &T,
                                                float k0, float k1, uint32_t *my, uint32_t &cnt, bool &full,
-                                               uint32_t *pack, const float *lds_pr) {
+                                               uint32_t *pack, const float *lds_pr, uint64_t bmask = ~0ull,
+                                               uint32_t bm_lo = 0u) {
     f2v ux = {T.ux, T.ux}, uy = {T.uy, T.uy}, uz = {T.uz, T.uz}, vy = {T.vy, T.vy};
     f2v vz = {T.vz, T.vz}, ku = {k0, k0}, kv = {k1, k1};
     const f2v th = {T.thr, T.thr};
@@ -560,6 +561,18 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
                 };
                 if (step(blk, b)) return b + 1;
             }
+        } else if (bmask != ~0ull) {
+            // the layer grid's blocks (hit_world_pre_ld: bit j = block bm_lo + j,
+            // wave-uniform; end <= bm_lo + 64): the set ones, in order
+            while (b < end) {
+                const uint64_t r = bmask & (~0ull << (b - bm_lo));
+                if (r == 0ull) break;
+                b = bm_lo + (uint32_t)__builtin_ctzll(r);
+                if (b >= end) break;
+                const cfloat_p blk = pre + 32 * b;
+                if (step([&](int i) { return blk[i]; }, b)) return b + 1;
+                ++b;
+            }
         } else {
             for (; b < end; ++b) {
                 const cfloat_p blk = pre + 32 * b;
@@ -578,7 +591,8 @@ __device__ __forceinline__ uint32_t scan_range(cfloat_p pre, uint32_t b, uint32_
 template <bool kPF, bool kTile = false>
 __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uint32_t nblk, const LineTest &T,
                                                    const KScene &S, uint32_t *list, uint32_t &cnt,
-                                                   uint32_t *pack = nullptr, const float *lds_pr = nullptr) {
+                                                   uint32_t *pack = nullptr, const float *lds_pr = nullptr,
+                                                   uint64_t gm = ~0ull) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
     const LineFlat K = line_test_flat(T, S.flat_cy);
@@ -587,7 +601,8 @@ __device__ __forceinline__ uint32_t scan_prefilter(cfloat_p pre, uint32_t b, uin
         if (b < S.flat_lo) {
             b = scan_range<kPF, false, kTile>(pre, b, min(S.flat_lo, nblk), T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         } else if (b < S.flat_hi) {
-            b = scan_range<kPF, true, kTile>(pre, b, min(S.flat_hi, nblk), T, K.ku, K.kv, my, cnt, full, pack, lds_pr);
+            b = scan_range<kPF, true, kTile>(pre, b, min(S.flat_hi, nblk), T, K.ku, K.kv, my, cnt, full, pack, lds_pr,
+                                             gm, S.flat_lo);
         } else {
             b = scan_range<kPF, false, kTile>(pre, b, nblk, T, T.nou, T.nov, my, cnt, full, pack, lds_pr);
         }
@@ -946,6 +961,33 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     return idx;
 }
 
+// The layer grid (rtx_grid.h): the blocks of the flat run some
+// lane of the wave may need — the OR of the lanes' walks. Only the lanes that
+// reach hit_world take part (an inactive lane needs nothing); the OR goes
+// through one LDS word per wave, the list's spare row at the wave's first two
+// lanes (`spare`: the list's row `cap`, never a list entry). A lane outside
+// the prefilter's safe range marks every block.
+#ifndef RTX_GRID  // A/B build: 0 = every block of the flat run is scanned
+#define RTX_GRID 1
+#endif
+__device__ __forceinline__ uint64_t grid_wave_mask(const KScene &S, f3 o, f3 d, const LineTest &T, uint32_t *spare) {
+    const LayerGrid G = *S.grid;  // wave-uniform: scalar loads
+    const uint64_t *gc = reinterpret_cast<const uint64_t *>(S.grid + 1);
+    const uint64_t mine = T.thr == -__uint_as_float(0x7f800000u)
+                              ? ~0ull
+                              : grid_mask(G, [gc](uint32_t k) { return gc[k]; }, o.x, o.y, o.z, d.x, d.y, d.z);
+    unsigned long long *w = reinterpret_cast<unsigned long long *>(spare + (threadIdx.x & ~63u));
+    const uint32_t lead = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x);
+    if (threadIdx.x == lead) __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_fetch_or(w, (unsigned long long)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // hit_world with the prefiltered scan: same (best, idx) as the in-order
 // reference scan. Candidates are resolved in rounds (a round ends when some
 // lane's list is full); the (min c, largest index) rule is
@@ -974,6 +1016,11 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
         T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
         T.thr = __uint_as_float(0x7f800000u);
     }
+    // the layer grid (small scenes, rtx_grid.h): the flat run's blocks some lane of the wave needs
+    uint64_t gm = ~0ull;
+    if constexpr (!kPF) {
+        if (RTX_GRID && S.grid != nullptr) gm = grid_wave_mask(S, o, d, T, list + cand_of<kPF>() * kRB);
+    }
     const float best0 = best;
     int idx = -1;
     bool ok = true;
@@ -985,7 +1032,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     uint32_t b = b0, end = nblk;
     for (;;) {
         uint32_t cnt;
-        b = scan_prefilter<kPF, kTile>(pre, b, end, T, S, list, cnt, pack, lds_pr);
+        b = scan_prefilter<kPF, kTile>(pre, b, end, T, S, list, cnt, pack, lds_pr, gm);
         ok = resolve_pre_t(ld, S.n, list, cnt, o, d, a, inv_a, t_min, best, idx, cand_of<kPF>()) && ok;
         if (b < end) continue;
         if (end == nblk && b0 != 0u) {  // wrap round to the start
@@ -2220,52 +2267,44 @@ constexpr uint32_t kBeatShift = 10;  // prom[4] holds s_memrealtime >> 10 (10.24
 __device__ __forceinline__ void flag_error(const KParams &P, uint32_t bit) {
     if (P.errors && (threadIdx.x & 63u) == 0u) atomicOr(P.errors, bit);
 }
-struct Valve {
-    unsigned long long t0, last, max_gap;
-    uint32_t polls, stalls;
+struct Valve {  // 32-bit s_memrealtime ticks (wrap after 42 s; the valve is shorter): few SGPRs in k_render
+    uint32_t t0, last, stalls;
     __device__ __forceinline__ void start() {
-        t0 = last = __builtin_amdgcn_s_memrealtime();
-        max_gap = 0ull;
-        polls = stalls = 0u;
+        t0 = last = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        stalls = 0u;
     }
-    __device__ __forceinline__ void progress() {  // a pixel written or a heartbeat seen
-        t0 = last;
-        max_gap = 0ull;
-        polls = 0u;
-    }
+    __device__ __forceinline__ void progress() { t0 = last; }  // a pixel written or a heartbeat seen
     // one poll; true once the server has polled on time for kPromValveTicks
     // since it last saw progress
     __device__ __forceinline__ bool expired() {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long gap = now - last;
-        last = now;
-        ++polls;
-        if (gap > kBeatTicks) {  // the server itself did not run: restart the clock
+        const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (now - last > (uint32_t)kBeatTicks) {  // the server itself did not run: restart the clock
             t0 = now;
             ++stalls;
-        } else if (gap > max_gap) {
-            max_gap = gap;
         }
-        return now - t0 > kPromValveTicks;
+        last = now;
+        return now - t0 > (uint32_t)kPromValveTicks;
     }
 };
+static_assert(kPromValveTicks < (1ull << 31), "the valve's 32-bit clock");
 // The valve fired: flag the launch and, if no server has yet, record what
-// this one saw (rtx_internal.h kErrDiagWords). Wave-uniform call.
-__device__ __noinline__ void valve_fire(const KParams &P, uint32_t bit, uint32_t who, const Valve &V, uint32_t target,
-                                        uint32_t npix, uint32_t entry) {
+// this one saw in one 64-bit word (rtx_internal.h KParams::err_diag; the host
+// adds the launch's queue counters, which stay in memory after it). Kept to
+// one atomic: the record's code sits in k_render, whose registers are tight
+// (a larger record moved the C2 render's spill code).
+#ifndef RTX_VALVE_RECORD  // A/B build: 0 = the error bit alone
+#define RTX_VALVE_RECORD 1
+#endif
+__device__ __forceinline__ void valve_fire(const KParams &P, uint32_t bit, uint32_t who, const Valve &V) {
     flag_error(P, bit);
-    if (P.err_diag == nullptr || (threadIdx.x & 63u) != 0u) return;
-    if (atomicCAS(P.err_diag, 0ull, (unsigned long long)(bit | who << 8)) != 0ull) return;
-    auto ld = [](const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    if (!RTX_VALVE_RECORD || P.err_diag == nullptr || (threadIdx.x & 63u) != 0u) return;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    unsigned long long *d = P.err_diag;
-    d[1] = now - V.t0;
-    d[2] = (uint32_t)((uint32_t)(now >> kBeatShift) - ld(&P.prom[4]));
-    d[3] = ld(&P.prom[0]) | (unsigned long long)ld(&P.prom[1]) << 32;
-    d[4] = ld(&P.prom[2]) | (unsigned long long)target << 32;
-    d[5] = ld(&P.prom[3]) | (unsigned long long)npix << 32;
-    d[6] = V.polls | (unsigned long long)V.stalls << 32;
-    d[7] = (uint32_t)min(V.max_gap, 0xffffffffull) | (unsigned long long)entry << 32;
+    const uint32_t bt = __hip_atomic_load(&P.prom[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t since = min(((uint32_t)now - V.t0) >> kBeatShift, 0xffffu);  // 10.24 us units
+    const uint32_t age = (uint32_t)(now >> kBeatShift) - bt;                    // the same units
+    const unsigned long long rec = (unsigned long long)(bit | who << 4 | min(V.stalls, 0xffu) << 8 | since << 16) |
+                                   (unsigned long long)age << 32;
+    atomicCAS(P.err_diag, 0ull, rec);
 }
 // The heartbeat (wave-uniform; `last` is the wave's previous beat).
 __device__ __forceinline__ void beat(const KParams &P, unsigned long long &last) {
@@ -2304,14 +2343,18 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
         if (got != ~0u) {
             const uint32_t *e = P.prom_q + 8u * got;
-            Valve E;  // the entry's producer publishes it right after claiming the slot: its own clock
-            E.start();
+            V.start();  // the entry's producer publishes it right after claiming the slot: a clock of its own
+            bool late = false;
             while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != P.epoch) {
                 __builtin_amdgcn_s_sleep(1);
-                if (E.expired()) {
-                    valve_fire(P, kErrPromEntryWait, 1u, E, target, npix, got);
-                    return false;
+                if (V.expired()) {
+                    late = true;
+                    break;
                 }
+            }
+            if (late) {
+                valve_fire(P, kErrPromEntryWait, 1u, V);
+                return false;
             }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the fields are read after the epoch matched
             W.gid = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2334,7 +2377,7 @@ __device__ __forceinline__ bool take_promoted(const KParams &P, const Frame &F, 
         }
         if (h >= t) __builtin_amdgcn_s_sleep(127);
         if (V.expired()) {
-            valve_fire(P, kErrPromTimeout, 1u, V, target, npix, ~0u);
+            valve_fire(P, kErrPromTimeout, 1u, V);
             return false;
         }
     }
@@ -2629,11 +2672,9 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
             if ((lb | tb) != 0ull) {
                 if (lb != 0ull) {
                     const uint32_t src = (uint32_t)__builtin_ctzll(lb);  // the record: the first late lane's wait
-                    E.t0 = __shfl(E.t0, (int)src, 64);
-                    E.polls = (uint32_t)__shfl((int)E.polls, (int)src, 64);
+                    E.t0 = (uint32_t)__shfl((int)E.t0, (int)src, 64);
                     E.stalls = (uint32_t)__shfl((int)E.stalls, (int)src, 64);
-                    E.max_gap = __shfl(E.max_gap, (int)src, 64);
-                    valve_fire(P, kErrPromEntryWait, 2u, E, target, npix, h + (uint32_t)__shfl((int)rank, (int)src, 64));
+                    valve_fire(P, kErrPromEntryWait, 2u, E);
                 }
                 if (tb != 0ull) flag_error(P, kErrPromTorn);
                 return -1;
@@ -2644,7 +2685,7 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_sleep(127);
         if (V.expired()) {
-            valve_fire(P, kErrPromTimeout, 2u, V, target, npix, ~0u);
+            valve_fire(P, kErrPromTimeout, 2u, V);
             return -1;
         }
     }

@@ -44,3 +44,47 @@ def test_prefilter_never_drops_a_reference_candidate(tmp_path):
     # slower), on the single-sphere cases, a fifth of them starting on the sphere
     assert rep["sphere_half_missed"] == 0 and rep["sphere_reference_accepted"] > 500_000, rep
     assert rep["sphere_half_max_used"] < 1.0 and rep["sphere_half_culled"] > 100_000, rep
+
+
+GRID_SRC = os.path.join(ROOT, "tests", "grid_check.cpp")
+
+
+def _build_grid_check(tmp_path, header_dir):
+    exe = str(tmp_path / "grid_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-mfma", "-I", header_dir, "-o", exe, GRID_SRC],
+                   check=True)
+    return exe
+
+
+def test_layer_grid_never_skips_an_accepted_sphere(tmp_path):
+    """The layer grid (rtx_grid.h): a block of the flat run is left out of a
+    wave's scan only if no lane's walk marks it; tests/grid_check.cpp checks,
+    on RTIOW and random layers and adversarial rays (near-tangent at every
+    slope down to grazing the layer, through cell corners, along the axes,
+    leaving a sphere's surface), that every sphere the reference accepts is
+    in a marked block. The checker itself must catch a grid built without
+    the margins (rho = r, no fattening)."""
+    exe = _build_grid_check(tmp_path, ROOT)
+    out = subprocess.run([exe, "300", "4000"], capture_output=True, text=True, timeout=120)
+    rep = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and rep["missed"] == 0, out.stderr
+    assert rep["accepted_spheres"] > 3_000_000 and rep["grid_applied"] > 900_000, rep
+    assert rep["every_block"] < 0.01 * rep["grid_applied"], rep  # the walk rarely gives up
+    # sensitivity: the same checker over a grid without the margins misses
+    bad = tmp_path / "bad" / "raytrace-we-gpu_amd" / "csrc"
+    bad.mkdir(parents=True)
+    src = open(os.path.join(ROOT, "raytrace-we-gpu_amd", "csrc", "rtx_grid.h")).read()
+    src = src.replace("constexpr double kGridFatCells = 1.0 / 256.0;", "constexpr double kGridFatCells = 0.0;")
+    src = src.replace(" + 27.0 * u * c2 + B) * (1.0 + 4.0 * u) * (1.0 + 1e-12)", ") * (1.0 - 1e-7)")
+    assert src.count("(1.0 - 1e-7)") == 2
+    (bad / "rtx_grid.h").write_text(src)
+    (bad / "rtx_prefilter.h").write_text(open(os.path.join(ROOT, "raytrace-we-gpu_amd", "csrc",
+                                                           "rtx_prefilter.h")).read())
+    btests = tmp_path / "bad" / "tests"
+    btests.mkdir()
+    (btests / "grid_check.cpp").write_text(open(GRID_SRC).read())
+    bexe = str(tmp_path / "grid_check_bad")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-mfma", "-o", bexe, str(btests / "grid_check.cpp")],
+                   check=True)
+    bout = subprocess.run([bexe, "300", "4000"], capture_output=True, text=True, timeout=120)
+    assert bout.returncode == 1 and json.loads(bout.stdout.strip().splitlines()[-1])["missed"] > 0

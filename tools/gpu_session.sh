@@ -30,6 +30,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     ubench) run ubench 120 ./tools/ubench_valu ;;
+    issue)  run issue 600 python tools/issue_probe.py ;;
     tests)  run tests 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 ;;
