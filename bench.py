@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--max-spheres", type=int, default=0)
     p.add_argument("--tile-rows", type=int, default=5)
     p.add_argument("--rng", choices=["chain", "per-sample"], default="chain")
+    p.add_argument("--scan", choices=["auto", "linear"], default="auto",
+                   help="hit_world's candidate search (rtx_set_scan_mode): auto = layer grid / culled scan, "
+                        "linear = every block of every segment (the reference's Hittable_list traversal)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
                    help="rocprofv3 PMC child passes for HBM traffic (rank 0, N=1)")
@@ -99,6 +102,7 @@ def probe(args):
     import rtx
     world, frame = scene_and_frame(args)
     with rtx.Context(0) as ctx:
+        ctx.set_scan_mode(args.scan)
         ctx.upload_world(world)
         ctx.set_frame(frame)
         if args.probe_scan:  # hit_world alone at the render's occupancy (rtx_debug_scan_rate)
@@ -119,7 +123,7 @@ def probe(args):
 def kernel_class(name):
     """The role of one dispatch of an rtx_render_rows launch (rocprof
     Kernel_Name), or None for the HIP runtime's own fills and copies."""
-    m = re.search(r"k_render<(true|false), (true|false), (true|false)>", name)
+    m = re.search(r"k_render<(true|false), (true|false), (true|false)(, (true|false))?>", name)
     if m:
         if m.group(2) == "true":
             return "prepass"
@@ -141,7 +145,8 @@ def _pmc_pass(args, counters, tag, rng=None, extra=()):
         raise RuntimeError("rocprofv3 not found")
     base = [sys.executable, os.path.abspath(__file__), "--probe", "--width", str(args.width),
             "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth),
-            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", rng or args.rng] + list(extra)
+            "--grid", str(args.grid), "--max-spheres", str(args.max_spheres), "--rng", rng or args.rng,
+            "--scan", args.scan] + list(extra)
     out = tempfile.mkdtemp(prefix=f"rtx_pmc_{tag}_")
     cmd = [exe, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", out, "-o", "pmc", "--"] + base
     try:
@@ -449,15 +454,21 @@ def host_cpu():
     return {"nproc": os.cpu_count(), "model": model}
 
 
-def launch_desc(n_spheres, spp, nparts, rng):
+def launch_desc(n_spheres, spp, nparts, rng, scan_mode="auto"):
     """What one rtx_render_rows launch runs for this configuration
     (rtx_kernels.hip launch_render / launch_ps)."""
     if spp < 8 and rng == "chain":
         return "rtx_render_rows launch = k_render<false> (exact grid, one lane per pixel)"
     large = ((n_spheres + 7) // 8) * 8 > 1024  # kScanPfMin: the kPF kernels
-    scan = ("culled scan over a spatially ordered copy of the scene (bounds over 512, 64 and 8 spheres, then spheres;"
-            " the coop tiers split the same hierarchy over a ray's lanes), candidate lists of 24"
-            if large else "scalar-loaded scan, resolve from the block's LDS copy of the scene")
+    if scan_mode == "linear":
+        scan = ("linear scan: every 8-sphere block of the scene for every segment, in index order "
+                + ("(streamed through a per-wave LDS tile of 64 blocks), candidate lists of 24" if large
+                   else "(scalar loads), resolve from the block's LDS copy of the scene"))
+    else:
+        scan = ("culled scan over a spatially ordered copy of the scene (bounds over 512, 64 and 8 spheres, then "
+                "spheres; the coop tiers split the same hierarchy over a ray's lanes), candidate lists of 24"
+                if large else "scalar-loaded scan of the flat layer's blocks the wave's slab walks mark (layer grid) "
+                              "and of every other block, resolve from the block's LDS copy of the scene")
     if rng == "per-sample":
         return f"k_render_ps (one lane per pixel-sample, in-order fold per pixel; {scan.split(' (')[0]})"
     whole = nparts == 1
@@ -620,6 +631,7 @@ def main():
     stream = torch.cuda.Stream(device=local_rank)
     torch.cuda.set_stream(stream)
     ctx = rtx.Context(local_rank, stream=stream.cuda_stream)
+    ctx.set_scan_mode(args.scan)
     ctx.upload_world(world)
     ctx.set_frame(frame)
     dev = torch.device("cuda", local_rank)
@@ -759,7 +771,7 @@ def main():
                           "executed": ps_exec,
                           "traffic": None if ps_traffic is None else round(ps_traffic), "pmc": ps_pmc,
                           "measured_hbm_GBs": None if ps_traffic is None else round(ps_traffic / (ps_ms * 1e-3) / 1e9, 3),
-                          "kernel": launch_desc(world.count, args.spp, R, "per-sample")}
+                          "kernel": launch_desc(world.count, args.spp, R, "per-sample", args.scan)}
             if args.cpu_seconds > 0:
                 rows_ps = [int(r) for r in np.linspace(5, H - 6, 16)]  # 16 rows spread over the image
                 per_sample["parity"] = per_sample_parity(world, frame, image.cpu().numpy(), rows_ps)
@@ -767,7 +779,7 @@ def main():
             ctx.set_frame(frame)
         roof = roofline_of(executed, launch_ms, tests_per_launch)
         roof.update(traffic=None if traffic is None else round(traffic),
-                    kernel=launch_desc(world.count, args.spp, R, args.rng), kernel_ms=round(launch_ms, 4),
+                    kernel=launch_desc(world.count, args.spp, R, args.rng, args.scan), kernel_ms=round(launch_ms, 4),
                     sphere_tests_per_launch=tests_per_launch,
                     segments_per_sample=round(st.segments / max(1, st.samples), 4),
                     pmc=pmc_note, executed=executed, issue_ceiling=ceiling)
@@ -785,9 +797,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic (deterministic RTIOW random_world scene, MSVC-rand LCG)",
             "config": {"workload": f"RTIOW final scene {W}x{H}, spp {args.spp}, depth {args.depth}, "
-                                   f"{world.count} spheres, {args.rng} RNG",
+                                   f"{world.count} spheres, {args.rng} RNG"
+                                   + (", linear scan" if args.scan == "linear" else ""),
                        "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                       "spheres": world.count, "rng": args.rng, "tile_rows": T,
+                       "spheres": world.count, "rng": args.rng, "scan": args.scan, "tile_rows": T,
                        "parallelism": f"row-tiles x{R}" + (" + RCCL gather" if collective else "")},
             "roofline": roof,
             "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 3),

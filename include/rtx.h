@@ -38,8 +38,10 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 143 /* 1.4.3 */
+#define RTX_VERSION 144 /* 1.4.4 */
 /* ABI notes.
+ *  1.4.4: rtx_set_scan_mode (RTX_SCAN_AUTO / RTX_SCAN_LINEAR; a new entry
+ *         point, no layout change).
  *  1.4.3: RTX_DEBUG_CULLED_COOP_LANE(q) (the culled coop's per-lane walk);
  *         RTX_ERR_INCOMPLETE's message names which promotion wait fired and
  *         what the server saw (no layout change).
@@ -286,6 +288,16 @@ RTX_API int rtx_get_schedule(rtx_ctx *ctx, rtx_schedule *out);
 /* ---- scene / frame upload ----------------------------------------------
  * ~ CreateBuffer(WorldDef, IMMUTABLE) (DxCSApp.cpp:393-413). */
 RTX_API int rtx_upload_world(rtx_ctx *ctx, const rtx_world *world);
+/* How hit_world finds its candidates (the answer is the reference's in both):
+ * RTX_SCAN_AUTO (the default): the flat layer's blocks through the layer grid
+ * (scenes up to 1,024 spheres) and the culled scan over a spatially ordered
+ * copy (larger scenes); RTX_SCAN_LINEAR: every block of the scene for every
+ * ray segment, in Hittable_list order (Hittable_list.cpp:3-20,
+ * ShaderCompute.hlsl:194), with the prefilter — large scenes stream it
+ * through a per-wave LDS tile of 64 blocks. Takes effect at the next
+ * rtx_upload_world. */
+enum { RTX_SCAN_AUTO = 0, RTX_SCAN_LINEAR = 1 };
+RTX_API int rtx_set_scan_mode(rtx_ctx *ctx, int mode);
 /* ~ Map(WRITE_DISCARD)/memcpy/Unmap of PerFrame (DxCSApp.cpp:494-496).
  * Host-side only: constants travel as kernel arguments. */
 RTX_API int rtx_set_frame(rtx_ctx *ctx, const rtx_frame *frame);

@@ -89,6 +89,7 @@ struct rtx_ctx {
     // layer grid of the flat run (small scenes; rtx_grid.h; none: null):
     // its LayerGrid, then the cells' block masks
     rtx::LayerGrid *d_grid = nullptr;
+    int scan_mode = RTX_SCAN_AUTO;  // rtx_set_scan_mode: applied by rtx_upload_world
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
     float4 *d_mval = nullptr;
@@ -702,12 +703,13 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
                               w->mat_values[4 * i + 2], w->mat_values[4 * i + 3]);
     }
     CullLayout cl;
-    const bool cull = RTX_CULL && n_pad > rtx::kScanPfMin;  // the large-scene (kPF) kernels scan it
+    const bool linear = c->scan_mode == RTX_SCAN_LINEAR;  // every block of every segment: no grid, no culled copy
+    const bool cull = RTX_CULL && !linear && n_pad > rtx::kScanPfMin;  // the large-scene (kPF) kernels scan it
     if (cull) cl = build_cull(w, pre4, flat_hi > flat_lo, flat_cy);
     // the small-scene lane-mode scan's layer grid over the flat run (rtx_grid.h)
     rtx::LayerGrid grid{};
     std::vector<unsigned long long> gcell;
-    const bool has_grid = RTX_GRID_UPLOAD && !cull && n_pad <= rtx::kScanPfMin && flat_hi > flat_lo &&
+    const bool has_grid = RTX_GRID_UPLOAD && !linear && n_pad <= rtx::kScanPfMin && flat_hi > flat_lo &&
                           rtx::build_layer_grid(w->spheres, 8 * flat_lo, std::min(8 * flat_hi, n), grid, gcell);
     RTX_HIP(hipStreamSynchronize(c->stream));
     free_world(c);
@@ -771,6 +773,13 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     c->depth = w->depth;
     c->spp = w->spp;
     c->have_world = true;
+    return RTX_OK;
+}
+
+int rtx_set_scan_mode(rtx_ctx *c, int mode) {
+    if (!c) return fail(RTX_ERR_INVALID, "rtx_set_scan_mode: null ctx");
+    if (mode != RTX_SCAN_AUTO && mode != RTX_SCAN_LINEAR) return fail(RTX_ERR_INVALID, "rtx_set_scan_mode: unknown mode");
+    c->scan_mode = mode;
     return RTX_OK;
 }
 

@@ -201,6 +201,11 @@ constexpr uint32_t kRB = 256;           // threads per render workgroup
 #define RTX_WAVES_PER_SIMD_PF (RTX_CULL ? 3 : 4)
 #endif
 #define RTX_RENDER_BOUNDS_T(kPF) __launch_bounds__(kRB, (kPF) ? RTX_WAVES_PER_SIMD_PF : RTX_WAVES_PER_SIMD)
+// kLin (the linear-scan mode, rtx_set_scan_mode: a large scene without the
+// culled layout scans every block through the per-wave LDS tile): 4 waves per
+// SIMD, what its LDS allows
+#define RTX_RENDER_BOUNDS_T2(kPF, kLin) \
+    __launch_bounds__(kRB, (kPF) ? ((kLin) ? 4 : RTX_WAVES_PER_SIMD_PF) : RTX_WAVES_PER_SIMD)
 #ifndef RTX_PS_WAVES_PF  // the per-sample kernel's large-scene instance (A/B: 4 = 128 VGPRs)
 #define RTX_PS_WAVES_PF RTX_WAVES_PER_SIMD
 #endif
@@ -2421,8 +2426,9 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
-template <bool kPersist, bool kCost = false, bool kPF = false>
-__global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
+template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false>
+__global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
+    constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][coop LDS copy of the spheres]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -2523,7 +2529,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
             unsigned long long *ctqp;
             unsigned long long *cp = D.coop_begin(H.tier, ctqp);
             bool promoted = false;
-            int my_hit = (kPF && RTX_CULL)
+            int my_hit = kCulled
                              ? hit_world_groups_culled(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws,
                                                        my_best, my_seq)
                          : coop_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin,
@@ -2559,7 +2565,7 @@ __global__ void RTX_RENDER_BOUNDS_T(kPF) k_render(const KParams P) {
         }
         bool promoted = false;
         D.rays(P, L.o, L.d, L.active, L.slot);
-        if (kPF && RTX_CULL) {  // large scenes: the culled scan (block bounds first, scan_culled)
+        if (kCulled) {  // large scenes: the culled scan (block bounds first, scan_culled)
             if (L.active) {
                 float best = __uint_as_float(0x7f800000u);
                 const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -3073,8 +3079,9 @@ __device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t
     output_pixel(P, px0 + po, acc);
 }
 
-template <bool kPF>
+template <bool kPF, bool kLin = false>
 __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
+    constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][batch slots, kPsStateBytes]
     //              [LDS copy of the spheres (n <= kCoopLds)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -3145,7 +3152,7 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
         if (exhausted && __popcll(act) <= kCoopMax) {  // the wave's last few samples: group coop
             __builtin_amdgcn_s_setprio(kTailPrio);
             bool seq = false;
-            hit = (kPF && RTX_CULL)  // (no breadth-first one-ray walk here: its registers cost this kernel 16 %, R9f)
+            hit = kCulled  // (no breadth-first one-ray walk here: its registers cost this kernel 16 %, R9f)
                       ? hit_world_groups_culled<false>(P.scene, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws,
                                                        best, seq)
                   : sph_lds ? hit_world_groups(P.scene, sl, act, L.active, L.o, L.d, L.a, L.inv_a, kTMin, coop_ws, best,
@@ -3157,7 +3164,7 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
-            hit = (kPF && RTX_CULL) ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+            hit = kCulled ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list)
                   : sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                     L.inv_a, kTMin, best, list)
                             : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -3436,33 +3443,41 @@ static hipError_t allow_lds(const void *kern, size_t lds) {
 // k_render with the SGPR double-buffered scan for scenes whose `pre` array
 // does not stay in the scalar cache (kScanPfMin).
 static bool use_pf(const KScene &s) { return s.n_pad > kScanPfMin; }
+// The linear-scan mode (rtx_set_scan_mode RTX_SCAN_LINEAR, or an RTX_CULL=0
+// build): a large scene uploaded without the culled layout; its kernels scan
+// every block of every segment (the reference's Hittable_list order of work,
+// with the prefilter), through the per-wave LDS tile in the chain render.
+static bool use_lin(const KScene &s) { return use_pf(s) && s.cpre == nullptr; }
 template <bool kPersist, bool kCost>
-static const void *render_fn(bool pf) {
-    return pf ? (const void *)k_render<kPersist, kCost, true> : (const void *)k_render<kPersist, kCost, false>;
+static const void *render_fn(const KScene &s) {
+    return !use_pf(s) ? (const void *)k_render<kPersist, kCost, false>
+           : use_lin(s) ? (const void *)k_render<kPersist, kCost, true, true>
+                        : (const void *)k_render<kPersist, kCost, true>;
 }
 template <bool kPersist, bool kCost>
-static void launch_k(bool pf, uint32_t blocks, size_t lds, hipStream_t stream, const KParams &a) {
-    if (pf)
-        hipLaunchKernelGGL((k_render<kPersist, kCost, true>), dim3(blocks), dim3(kRB), lds, stream, a);
-    else
+static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t stream, const KParams &a) {
+    if (!use_pf(s))
         hipLaunchKernelGGL((k_render<kPersist, kCost, false>), dim3(blocks), dim3(kRB), lds, stream, a);
+    else if (use_lin(s))
+        hipLaunchKernelGGL((k_render<kPersist, kCost, true, true>), dim3(blocks), dim3(kRB), lds, stream, a);
+    else
+        hipLaunchKernelGGL((k_render<kPersist, kCost, true>), dim3(blocks), dim3(kRB), lds, stream, a);
 }
 
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    return (use_pf(s) ? list_bytes<true>() + 16 + (RTX_CULL ? 0u : kPfLdsBytes) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
+    return (use_pf(s) ? list_bytes<true>() + 16 + (use_lin(s) ? kPfLdsBytes : 0u) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
            (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0 || p.spp == 0 || p.depth == 0 || !p.cost_out) return hipErrorInvalidValue;
-    const bool pf = use_pf(p.scene);
     const size_t lds = render_lds(p.scene);
-    hipError_t e = allow_lds(render_fn<false, true>(pf), lds);
+    hipError_t e = allow_lds(render_fn<false, true>(p.scene), lds);
     if (e != hipSuccess) return e;
-    launch_k<false, true>(pf, ceil_div(lanes, kRB), lds, stream, p);
+    launch_k<false, true>(p.scene, ceil_div(lanes, kRB), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -3480,14 +3495,16 @@ static size_t ps_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
            (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
-static const void *ps_fn(bool pf) { return pf ? (const void *)k_render_ps<true> : (const void *)k_render_ps<false>; }
+static const void *ps_fn(const KScene &s) {
+    return !use_pf(s) ? (const void *)k_render_ps<false>
+           : use_lin(s) ? (const void *)k_render_ps<true, true> : (const void *)k_render_ps<true>;
+}
 static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
 // Every resident wave (an item is a sample, not a pixel: a frame share with
 // fewer pixels than lanes still fills the GPU), fewer only for tiny frames.
 static uint32_t ps_waves(const KParams &p) {
-    const bool pf = use_pf(p.scene);
     const uint64_t items = (uint64_t)p.rows_local * p.width * p.spp;
-    const uint32_t blocks = min(ceil_div(items, kRB), resident_blocks(ps_fn(pf), ps_lds(p.scene)));
+    const uint32_t blocks = min(ceil_div(items, kRB), resident_blocks(ps_fn(p.scene), ps_lds(p.scene)));
     return blocks * (kRB / 64);
 }
 size_t ps_scratch_floats(const KParams &p) {
@@ -3495,9 +3512,8 @@ size_t ps_scratch_floats(const KParams &p) {
     return (size_t)ps_waves(p) * kPsSlots * 4 * ps_cap_of(p.spp);
 }
 static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_t stream) {
-    const bool pf = use_pf(p.scene);
     const size_t lds = ps_lds(p.scene);
-    hipError_t e = allow_lds(ps_fn(pf), lds);
+    hipError_t e = allow_lds(ps_fn(p.scene), lds);
     if (e != hipSuccess) return e;
     const uint32_t waves = ps_waves(p);
     KParams q = p;
@@ -3512,10 +3528,12 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint32_t blocks = waves / (kRB / 64);
-    if (pf)
-        hipLaunchKernelGGL(k_render_ps<true>, dim3(blocks), dim3(kRB), lds, stream, q);
-    else
+    if (!use_pf(p.scene))
         hipLaunchKernelGGL(k_render_ps<false>, dim3(blocks), dim3(kRB), lds, stream, q);
+    else if (use_lin(p.scene))
+        hipLaunchKernelGGL((k_render_ps<true, true>), dim3(blocks), dim3(kRB), lds, stream, q);
+    else
+        hipLaunchKernelGGL(k_render_ps<true>, dim3(blocks), dim3(kRB), lds, stream, q);
     return hipGetLastError();
 }
 
@@ -3537,13 +3555,13 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     if (p.rng_mode == 1u) return launch_ps(p, sched, stream);  // one lane per (pixel, sample)
     const bool pf = use_pf(p.scene);
     const size_t lds = render_lds(p.scene);
-    hipError_t e = allow_lds(render_fn<true, false>(pf), lds);
-    if (e == hipSuccess) e = allow_lds(render_fn<false, false>(pf), lds);
-    if (e == hipSuccess) e = allow_lds(render_fn<false, true>(pf), lds);
-    if (e == hipSuccess) e = allow_lds(render_fn<true, true>(pf), lds);
+    hipError_t e = allow_lds(render_fn<true, false>(p.scene), lds);
+    if (e == hipSuccess) e = allow_lds(render_fn<false, false>(p.scene), lds);
+    if (e == hipSuccess) e = allow_lds(render_fn<false, true>(p.scene), lds);
+    if (e == hipSuccess) e = allow_lds(render_fn<true, true>(p.scene), lds);
     if (e != hipSuccess) return e;
     if (!sched.cost || p.spp < kLptMinSpp) {
-        launch_k<false, false>(pf, need, lds, stream, p);
+        launch_k<false, false>(p.scene, need, lds, stream, p);
         return hipGetLastError();
     }
     if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
@@ -3555,7 +3573,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     c.spp = min(p.spp, pf ? kCostSppLarge : kCostSpp);
     uint32_t split_cap = 0;
     {
-        const uint32_t rb = resident_blocks(render_fn<true, false>(pf), lds);
+        const uint32_t rb = resident_blocks(render_fn<true, false>(p.scene), lds);
         const bool whole = (double)lanes >= tune.rho2 * (double)min(need, rb) * kRB;  // a large part (the tiers' class)
         // a row-split share (small scenes) may cap too (cap_split): its stopped
         // pixels take the top bucket (tier 1), their neighbours count the cap
@@ -3579,15 +3597,15 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         // ends takes the next one), so the pass does not wait on each wave's
         // slowest pixel — at 100k spheres an exact grid spent 27 % of the
         // C5 frame here; for small scenes the exact grid measured ~1 % faster
-        const uint32_t pblocks = min(need, resident_blocks(render_fn<true, true>(pf), lds));
+        const uint32_t pblocks = min(need, resident_blocks(render_fn<true, true>(p.scene), lds));
         // its tail: once at most pre_stop pixels are in flight they stop (pre_stop)
         if (kPreStopFrac > 0.0) {
             c.pre_done = sched.buckets + 2 * kCostBuckets + 6;  // heavy[6], zeroed above
             c.pre_stop = (uint32_t)(kPreStopFrac * (double)pblocks * kRB);
         }
-        launch_k<true, true>(pf, pblocks, lds, stream, c);
+        launch_k<true, true>(p.scene, pblocks, lds, stream, c);
     } else {
-        launch_k<false, true>(pf, need, lds, stream, c);
+        launch_k<false, true>(p.scene, need, lds, stream, c);
     }
     // 2. counting sort by cost, descending
     const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
@@ -3595,7 +3613,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
                        p.rows_local, c.spp, split_cap, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
-    uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(pf), lds));
+    uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(p.scene), lds));
     {
         const double px_per_lane = (double)lanes / ((double)blocks * kRB);
         const double occ = px_per_lane < tune.rho ? tune.occ_small : px_per_lane < tune.rho_low ? tune.occ_low : tune.occ_normal;
@@ -3670,7 +3688,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         if (e != hipSuccess) return e;
         blocks = max(1u, blocks - (trace_waves + 3u) / 4u);
     }
-    launch_k<true, false>(pf, blocks, lds, stream, q);
+    launch_k<true, false>(p.scene, blocks, lds, stream, q);
     e = hipGetLastError();
     if (e == hipSuccess && trace_waves > 0) e = hipStreamWaitEvent(stream, sched.ev_join, 0);
     if (e == hipSuccess && sched.stage) {

@@ -46,6 +46,7 @@ def DEBUG_CULLED_COOP_LANE(q: int) -> int:
     return 0xFFFFFE00 | q
 MAT_LAMBERT, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
 RNG_CHAIN, RNG_PER_SAMPLE = 0, 1
+SCAN_MODES = {"auto": 0, "linear": 1}  # rtx_set_scan_mode (RTX_SCAN_AUTO / RTX_SCAN_LINEAR)
 FN = dict(sqrt=0, div=1, sin=2, cos=3, log2=4, exp2=5, pow=6, basehash=7,
           hash1=8, hash2=9, hash3=10, rius=11, lambert_dir=12, lambert_dir_guard=13)
 FRAME_LAMBERT_GUARD = 1  # rtx_frame.flags bit (RTX_FRAME_LAMBERT_GUARD)
@@ -120,6 +121,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
         "rtx_set_stream": (C.c_int, [ctx, vp]),
         "rtx_use_own_stream": (C.c_int, [ctx]),
         "rtx_upload_world": (C.c_int, [ctx, C.POINTER(rtx_world)]),
+        "rtx_set_scan_mode": (C.c_int, [ctx, C.c_int]),
         "rtx_set_frame": (C.c_int, [ctx, C.POINTER(rtx_frame)]),
         "rtx_render_rows": (C.c_int, [ctx, u32, u32, u32, vp]),
         "rtx_render": (C.c_int, [ctx]),
@@ -158,7 +160,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     # entry points added after 1.0 may be absent from older builds (A/B runs
     # of earlier libraries); calling one then fails with AttributeError
     optional = {"rtx_schedule_defaults", "rtx_set_schedule", "rtx_get_schedule", "rtx_debug_hit_world_from",
-                "rtx_build_info", "rtx_debug_scan_rate"}
+                "rtx_build_info", "rtx_debug_scan_rate", "rtx_set_scan_mode"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(lib, name):
             continue
@@ -358,6 +360,12 @@ class Context:
             _check(self._lib.rtx_use_own_stream(self._h), "rtx_use_own_stream", self._lib)
         else:
             _check(self._lib.rtx_set_stream(self._h, C.c_void_p(stream)), "rtx_set_stream", self._lib)
+
+    def set_scan_mode(self, mode: str):
+        """"auto" (layer grid / culled scan) or "linear" (every block of every
+        segment, Hittable_list order): rtx_set_scan_mode, applied by the next
+        upload_world."""
+        _check(self._lib.rtx_set_scan_mode(self._h, SCAN_MODES[mode]), "rtx_set_scan_mode", self._lib)
 
     def upload_world(self, world: World):
         w = world.as_struct()

@@ -1298,3 +1298,42 @@ def test_debug_scan_rate_probe(gpu_ctx, rtx):
     gpu_ctx.upload_world(big)
     with pytest.raises(rtx.RtxError):
         gpu_ctx.debug_scan_rate(1)
+
+
+@pytest.mark.parametrize("ctx_name", ["gpu_ctx", "stress_ctx"])
+@pytest.mark.parametrize("grid,spp", [(11, 12), (20, 6)])
+def test_scan_modes_bit_exact(request, oracle, rtx, ctx_name, grid, spp):
+    """rtx_set_scan_mode: the same frame through the default search (the layer
+    grid at 486 spheres, the culled scan at 1,600) and through the linear
+    scan (every block of every segment, the reference's Hittable_list order
+    of work; the large scene streams it through the per-wave LDS tile):
+    both bit for bit against the oracle, with equal segment counts, whole
+    frame and a 3-way share. The context goes back to the default mode."""
+    ctx = request.getfixturevalue(ctx_name)
+    world = rtx.random_world(grid, depth=50, spp=spp)
+    W, H, T = 256, 144, 4
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    rows = np.linspace(1, H - 2, 6).astype(np.uint32)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    try:
+        for mode in ("linear", "auto"):
+            ctx.set_scan_mode(mode)
+            ctx.upload_world(world)
+            ctx.set_frame(frame)
+            ctx.stats_reset()
+            img = ctx.render_image()
+            segs = ctx.stats().segments
+            assert_bits_equal(img[rows], want, f"{ctx_name} grid {grid} {mode}")
+            if mode == "linear":
+                ref_img, ref_segs = img, segs
+            else:
+                assert segs == ref_segs
+                assert_bits_equal(img, ref_img, f"{ctx_name} grid {grid}: auto vs linear")
+            ids = rtx.part_row_ids(H, T, 1, 3)
+            buf = ctx.alloc((len(ids), W, 4))
+            ctx.render_rows(T, 1, 3, buf.ptr)
+            got = buf.numpy()
+            buf.free()
+            assert_bits_equal(got, ref_img[ids], f"{ctx_name} grid {grid} {mode}: share 1 of 3")
+    finally:
+        ctx.set_scan_mode("auto")

@@ -47,6 +47,8 @@ for s in $STEPS; do
     c3b)    run c3b 900 python bench.py --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 --parts '' ;;
     c5b)    run c5b 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --parts '' --per-sample ${C5PS:-0} ;;
     c3ps)   run c3ps 900 python bench.py --rng per-sample --width 3840 --height 2160 --spp 1024 --steps 2 --warmup 1 --cpu-seconds 10 --parts '' ;;
+    c5lin)  run c5lin 900 python bench.py --spp 16 --grid 159 --max-spheres 100000 --scan linear --steps 1 --warmup 1 --cpu-seconds 10 --parts '' --per-sample 0 ;;
+    c2lin)  run c2lin 600 python bench.py --scan linear --steps 5 --warmup 1 --cpu-seconds 10 --parts '' --per-sample 0 ;;
     c5ps)   run c5ps 900 python bench.py --rng per-sample --spp 16 --grid 159 --max-spheres 100000 --steps 3 --warmup 1 --cpu-seconds 10 --parts '' ;;
     variants) run variants 900 python tools/variant_bench.py --rounds ${VROUNDS:-5} --frames 2 ${VARGS:-} ${VNAMES:-} ;;
     ctrlist) run ctrlist 120 rocprofv3 -L ;;
