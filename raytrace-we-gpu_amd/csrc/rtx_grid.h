@@ -49,6 +49,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <utility>
+#include <vector>
 
 #if defined(__HIPCC__)
 #define RTX_GD __host__ __device__ __forceinline__
@@ -61,27 +63,45 @@ namespace rtx {
 constexpr float kGridOMax = 64.0f;      // rays with |o| above this scan every block
 constexpr double kGridFatCells = 1.0 / 256.0;  // cell-list fattening, in cells
 constexpr double kGridSlabPad = 1e-3;          // slab half-width past rho_max (y units)
-constexpr uint32_t kGridMaxSteps = 48;  // a longer walk scans every block
-constexpr uint32_t kGridMaxCells = 4096;
+constexpr uint32_t kGridMaxSteps = 48;  // a longer walk (the block-mask grid) scans every block
+constexpr uint32_t kGridMaxCells = 4096;  // the block-mask grid (small scenes)
+constexpr uint32_t kGridListSlots = 4;    // the block-list grid (large scenes): block ids per cell
+constexpr uint16_t kGridNone = 0xffffu;   // ... an empty slot
+constexpr uint16_t kGridFull = 0xfffeu;   // ... the cell needs more blocks than it holds: every block
+constexpr uint32_t kGridListCap = 256;     // blocks a wave's union lists (rtx_kernels.hip grid_union)
+constexpr uint32_t kGridMaxStepsLarge = 96;  // a longer walk (the block-list grid) takes the culled scan
+// LDS words per wave of the block-list grid's union: length, spare, bitmap, list
+RTX_GD constexpr uint32_t grid_ws_words(uint32_t nblk_flat) { return 2u + (nblk_flat + 31u) / 32u + kGridListCap / 2u; }
 
 struct LayerGrid {
     float x0, z0;      // the grid's corner (multiples of h)
     float h, inv_h;    // cell side (a power of two) and its inverse (exact)
     float ylo, yhi;    // the slab: y0 -+ (rho_max + kGridSlabPad), rounded outwards
     uint32_t nx, nz;   // cells along x and z; cell (ix, iz) covers [x0 + ix h, x0 + (ix + 1) h] x ...
+    float far_m;       // far cut: the walk may stop kGridFar(...) past the best root so far (distance units)
+    uint32_t nblk;     // blocks the cells name (the block-list grid's bitmap size; the mask grid: <= 64)
 };
 
-// The walk: the mask of the flat run's blocks the ray (o, d) may need
-// (bit j: block flat_lo + j); ~0 when the lane must scan every block.
-// `cell(k)` returns cell k's mask (k = ix * nz + iz).
-template <typename Cell>
-RTX_GD uint64_t grid_mask(const LayerGrid &G, Cell cell, float ox, float oy, float oz, float dx, float dy, float dz) {
-    const uint64_t all = ~0ull;
+// The far cut (the block-list grid). A walk that knows the
+// ray's best root B so far (the non-flat part of the scene resolved first)
+// need only reach t = B + far_m / |d|: a sphere the reference accepts at a
+// root c <= B has a point of its rho-ball chord at t <= c + e, e the fp32
+// root's error, <= 2 sqrt(8u) |o - c_i| / |d| (the discriminant's rounding,
+// 8u (hb^2 + a|cc|), through the square root) — far_m = 4e-3 (|o|max +
+// |c|max) + 1e-3 covers it with a factor >= 2.8; tests/grid_check.cpp checks
+// the cut with B at the winner's own root (ties go to the later sphere).
+// The walk: visits the cells (k = ix * nz + iz) the (x, z) projection of the
+// ray's stretch inside the slab and the grid's box, t in [0, t_stop], crosses;
+// returns false when it gives up (far or non-finite ray, or more than
+// max_steps cells): the caller then scans every block.
+template <typename Visit>
+RTX_GD bool grid_walk(const LayerGrid &G, uint32_t max_steps, float ox, float oy, float oz, float dx, float dy,
+                      float dz, float t_stop, Visit visit) {
     const float o2 = fmaf(ox, ox, fmaf(oy, oy, oz * oz));
     const float d2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-    if (!(o2 <= kGridOMax * kGridOMax) || !(d2 <= 3.0e38f)) return all;  // far or non-finite: every block
+    if (!(o2 <= kGridOMax * kGridOMax) || !(d2 <= 3.0e38f)) return false;  // far or non-finite
     const float inf = INFINITY;
-    float t0 = 0.0f, t1 = inf;
+    float t0 = 0.0f, t1 = t_stop >= 0.0f ? t_stop : inf;  // (NaN t_stop: no cut)
     // the slab and the grid's box, one axis at a time: [lo, hi] along o + t d
     auto clip = [&](float o, float d, float lo, float hi) {
         if (d == 0.0f) {
@@ -96,50 +116,67 @@ RTX_GD uint64_t grid_mask(const LayerGrid &G, Cell cell, float ox, float oy, flo
     clip(oy, dy, G.ylo, G.yhi);
     clip(ox, dx, G.x0, G.x0 + (float)G.nx * G.h);
     clip(oz, dz, G.z0, G.z0 + (float)G.nz * G.h);
-    if (!(t0 <= t1)) return 0ull;  // the ray's t >= 0 part never enters the slab inside the grid
+    if (!(t0 <= t1)) return true;  // the ray's t >= 0 part never enters the slab inside the grid
     // start cell: the rounded point at t0 (clamped: it is within rounding of the box)
     const float sx = (fmaf(t0, dx, ox) - G.x0) * G.inv_h, sz = (fmaf(t0, dz, oz) - G.z0) * G.inv_h;
     int ix = (int)fminf(fmaxf(floorf(sx), 0.0f), (float)(G.nx - 1));
     int iz = (int)fminf(fmaxf(floorf(sz), 0.0f), (float)(G.nz - 1));
     const int stx = dx > 0.0f ? 1 : -1, stz = dz > 0.0f ? 1 : -1;
     const float ivx = dx == 0.0f ? 0.0f : 1.0f / dx, ivz = dz == 0.0f ? 0.0f : 1.0f / dz;
-    uint64_t m = 0ull;
-    for (uint32_t k = 0; k < kGridMaxSteps; ++k) {
-        m |= cell((uint32_t)ix * G.nz + (uint32_t)iz);
+    for (uint32_t k = 0; k < max_steps; ++k) {
+        if (!visit((uint32_t)ix * G.nz + (uint32_t)iz)) return false;
         // the next boundary crossings, each from its boundary (exact: a multiple of h)
         const float bx = fmaf((float)(ix + (dx > 0.0f ? 1 : 0)), G.h, G.x0);
         const float bz = fmaf((float)(iz + (dz > 0.0f ? 1 : 0)), G.h, G.z0);
         const float tx = dx == 0.0f ? inf : (bx - ox) * ivx;
         const float tz = dz == 0.0f ? inf : (bz - oz) * ivz;
-        if (!(fminf(tx, tz) <= t1)) return m;
+        if (!(fminf(tx, tz) <= t1)) return true;
         if (tx <= tz) {
             ix += stx;
-            if (ix < 0 || ix >= (int)G.nx) return m;
+            if (ix < 0 || ix >= (int)G.nx) return true;
         } else {
             iz += stz;
-            if (iz < 0 || iz >= (int)G.nz) return m;
+            if (iz < 0 || iz >= (int)G.nz) return true;
         }
     }
-    return all;
+    return false;
 }
 
-// Host: the grid of the spheres [i_lo, i_hi) of `sph` ((cx, cy, cz, r) per
-// sphere, every cy equal: y0), bit (i - i_lo) / 8 of a cell mask. Returns
-// false (no grid) if the run spans more than 64 blocks or the grid would
-// exceed kGridMaxCells cells. `cell` receives nx * nz masks.
-template <typename Vec>
-inline bool build_layer_grid(const float *sph, uint32_t i_lo, uint32_t i_hi, LayerGrid &G, Vec &cell) {
-    const uint32_t m = i_hi - i_lo;
-    if (m == 0 || (m + 7) / 8 > 64) return false;
+// The block-mask grid (small scenes): the mask of the flat run's blocks the
+// ray (o, d) may need (bit j: block flat_lo + j); ~0 when the lane must scan
+// every block. `cell(k)` returns cell k's mask.
+template <typename Cell>
+RTX_GD uint64_t grid_mask(const LayerGrid &G, Cell cell, float ox, float oy, float oz, float dx, float dy, float dz,
+                          float t_stop = INFINITY) {
+    uint64_t m = 0ull;
+    const bool done = grid_walk(G, kGridMaxSteps, ox, oy, oz, dx, dy, dz, t_stop, [&](uint32_t k) {
+        m |= cell(k);
+        return true;
+    });
+    return done ? m : ~0ull;
+}
+
+// Host: the geometry of a layer grid over `m` spheres sph[4 j] = (cx, cy,
+// cz, r) (every cy equal: y0) and, for each, every cell its disc of radius
+// rho_j + kGridFat meets: add(cell, j). Returns false (no grid) past
+// max_cells cells.
+template <typename Add>
+inline bool build_layer_grid_cells(const float *sph, uint32_t m, uint32_t max_cells, LayerGrid &G, Add add) {
+    if (m == 0) return false;
     const double u = 5.9604644775390625e-08;
-    const double y0 = sph[4 * (size_t)i_lo + 1];
+    const double y0 = sph[1];
     const double B = 26.0 * u * (double)kGridOMax * (double)kGridOMax;
-    double rho_max = 0.0, xlo = INFINITY, xhi = -INFINITY, zlo = INFINITY, zhi = -INFINITY;
-    for (uint32_t i = i_lo; i < i_hi; ++i) {
-        const double cx = sph[4 * (size_t)i], cz = sph[4 * (size_t)i + 2], r = sph[4 * (size_t)i + 3];
+    auto rho_of = [&](uint32_t j) {
+        const double cx = sph[4 * (size_t)j], cz = sph[4 * (size_t)j + 2], r = sph[4 * (size_t)j + 3];
         const double c2 = cx * cx + y0 * y0 + cz * cz;
-        const double rho = std::sqrt(r * r * (1.0 + 8.0 * u) + 27.0 * u * c2 + B) * (1.0 + 4.0 * u) * (1.0 + 1e-12);
+        return std::sqrt(r * r * (1.0 + 8.0 * u) + 27.0 * u * c2 + B) * (1.0 + 4.0 * u) * (1.0 + 1e-12);
+    };
+    double rho_max = 0.0, cmax = 0.0, xlo = INFINITY, xhi = -INFINITY, zlo = INFINITY, zhi = -INFINITY;
+    for (uint32_t j = 0; j < m; ++j) {
+        const double cx = sph[4 * (size_t)j], cz = sph[4 * (size_t)j + 2];
+        const double rho = rho_of(j);
         rho_max = std::fmax(rho_max, rho);
+        cmax = std::fmax(cmax, std::sqrt(cx * cx + y0 * y0 + cz * cz));
         xlo = std::fmin(xlo, cx - rho), xhi = std::fmax(xhi, cx + rho);
         zlo = std::fmin(zlo, cz - rho), zhi = std::fmax(zhi, cz + rho);
     }
@@ -151,20 +188,17 @@ inline bool build_layer_grid(const float *sph, uint32_t i_lo, uint32_t i_hi, Lay
     // the box: a spare cell on every side (no disc reaches it)
     const double x0 = (std::floor((xlo - fat) / h) - 1.0) * h, z0 = (std::floor((zlo - fat) / h) - 1.0) * h;
     const double nxd = std::ceil((xhi + fat - x0) / h) + 1.0, nzd = std::ceil((zhi + fat - z0) / h) + 1.0;
-    if (nxd * nzd > kGridMaxCells || !(std::fabs(x0) < 1e6 && std::fabs(z0) < 1e6)) return false;
+    if (nxd * nzd > max_cells || !(std::fabs(x0) < 1e6 && std::fabs(z0) < 1e6)) return false;
     G.nx = (uint32_t)nxd, G.nz = (uint32_t)nzd;
     G.h = (float)h, G.inv_h = (float)(1.0 / h);
     G.x0 = (float)x0, G.z0 = (float)z0;
     const double slab = rho_max + kGridSlabPad;
     G.ylo = nextafterf((float)(y0 - slab), -INFINITY);
     G.yhi = nextafterf((float)(y0 + slab), INFINITY);
-    cell.assign((size_t)G.nx * G.nz, 0ull);
-    for (uint32_t i = i_lo; i < i_hi; ++i) {
-        const double cx = sph[4 * (size_t)i], cz = sph[4 * (size_t)i + 2], r = sph[4 * (size_t)i + 3];
-        const double c2 = cx * cx + y0 * y0 + cz * cz;
-        const double rho =
-            std::sqrt(r * r * (1.0 + 8.0 * u) + 27.0 * u * c2 + B) * (1.0 + 4.0 * u) * (1.0 + 1e-12) + fat;
-        const uint64_t bit = 1ull << ((i - i_lo) / 8);
+    G.far_m = nextafterf((float)(4e-3 * ((double)kGridOMax + cmax) + 1e-3), INFINITY);
+    for (uint32_t j = 0; j < m; ++j) {
+        const double cx = sph[4 * (size_t)j], cz = sph[4 * (size_t)j + 2];
+        const double rho = rho_of(j) + fat;
         const int ax = (int)std::floor((cx - rho - x0) / h), bxi = (int)std::floor((cx + rho - x0) / h);
         const int az = (int)std::floor((cz - rho - z0) / h), bzi = (int)std::floor((cz + rho - z0) / h);
         for (int ix = std::max(ax, 0); ix <= std::min(bxi, (int)G.nx - 1); ++ix)
@@ -172,8 +206,55 @@ inline bool build_layer_grid(const float *sph, uint32_t i_lo, uint32_t i_hi, Lay
                 // the closed square's nearest point to the centre
                 const double qx = std::fmin(std::fmax(cx, x0 + ix * h), x0 + (ix + 1) * h);
                 const double qz = std::fmin(std::fmax(cz, z0 + iz * h), z0 + (iz + 1) * h);
-                if ((qx - cx) * (qx - cx) + (qz - cz) * (qz - cz) <= rho * rho) cell[(size_t)ix * G.nz + iz] |= bit;
+                if ((qx - cx) * (qx - cx) + (qz - cz) * (qz - cz) <= rho * rho) add((uint32_t)ix * G.nz + iz, j);
             }
+    }
+    return true;
+}
+
+// Host: the block-mask grid of the spheres [i_lo, i_hi) of `sph` (bit
+// (i - i_lo) / 8 of a cell's mask). Returns false (no grid) if the run spans
+// more than 64 blocks or the grid would exceed kGridMaxCells cells. `cell`
+// receives nx * nz masks.
+template <typename Vec>
+inline bool build_layer_grid(const float *sph, uint32_t i_lo, uint32_t i_hi, LayerGrid &G, Vec &cell) {
+    const uint32_t m = i_hi - i_lo;
+    if (m == 0 || (m + 7) / 8 > 64) return false;
+    std::vector<std::pair<uint32_t, uint32_t>> hits;
+    if (!build_layer_grid_cells(sph + 4 * (size_t)i_lo, m, kGridMaxCells, G,
+                                [&](uint32_t k, uint32_t j) { hits.emplace_back(k, j); }))
+        return false;
+    G.nblk = (m + 7) / 8;
+    cell.assign((size_t)G.nx * G.nz, 0ull);
+    for (const auto &h : hits) cell[h.first] |= 1ull << (h.second / 8);
+    return true;
+}
+
+// Host: the block-list grid (large scenes): m spheres sph[4 j], sphere j in
+// block blk[j] (< 0xfffe); per cell kGridListSlots block ids (kGridNone: an
+// empty slot; kGridFull in slot 0: the cell names more blocks than it holds,
+// a walk through it scans every block).
+inline bool build_layer_grid_blocks(const float *sph, const uint32_t *blk, uint32_t m, uint32_t max_cells,
+                                    LayerGrid &G, std::vector<uint16_t> &slots) {
+    std::vector<std::pair<uint32_t, uint32_t>> hits;
+    if (!build_layer_grid_cells(sph, m, max_cells, G, [&](uint32_t k, uint32_t j) { hits.emplace_back(k, j); }))
+        return false;
+    uint32_t nb = 0;
+    for (uint32_t j = 0; j < m; ++j) nb = std::max(nb, blk[j] + 1u);
+    if (nb >= kGridFull) return false;
+    G.nblk = nb;
+    slots.assign((size_t)G.nx * G.nz * kGridListSlots, kGridNone);
+    for (const auto &h : hits) {
+        uint16_t *s = &slots[(size_t)h.first * kGridListSlots];
+        const uint16_t b = (uint16_t)blk[h.second];
+        if (s[0] == kGridFull) continue;
+        uint32_t q = 0;
+        while (q < kGridListSlots && s[q] != kGridNone && s[q] != b) ++q;
+        if (q == kGridListSlots) {
+            s[0] = kGridFull;  // overflow
+            continue;
+        }
+        s[q] = b;
     }
     return true;
 }

@@ -743,12 +743,17 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // group is tested again, its earlier blocks masked off). Wave-uniform.
 // A bound also fails when it is wholly behind the lane's origin (the half
 // test H, Hs: rtx_prefilter.h HalfTest; 5 more fp32 ops per bound, 4 flat).
-__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, const LineTest &Ts,
-                                                const HalfTest &H, const HalfTest &Hs, uint32_t *list,
-                                                uint32_t &cnt) {
+// `end` (a multiple of 512 blocks, or the layout's end): the scan stops there.
+// `wl` (the grid's union of the wave's walks, wn flat-section blocks relative
+// to cflat_lo, GridWs): the scan visits those blocks instead of the hierarchy,
+// b then being the list position to resume at.
+__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, uint32_t end, const LineTest &T,
+                                                const LineTest &Ts, const HalfTest &H, const HalfTest &Hs,
+                                                uint32_t *list, uint32_t &cnt, const uint16_t *wl = nullptr,
+                                                uint32_t wn = 0u) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
-    const uint32_t nblk = S.n_cpad / 8u;
+    const uint32_t nblk = min(S.n_cpad / 8u, end);
     const LineFlat K = line_test_flat(T, S.flat_cy);
     // flat bounds: the ray stretched along y (rtx_prefilter.h kCullSy), the 5-op test
     const LineFlat Ks = line_test_flat(Ts, kCullSy * S.flat_cy);
@@ -888,13 +893,20 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, con
     // stretched) iff b0 >= cflat_lo (cflat_lo is a multiple of 512 blocks, so
     // no test straddles it: rtx_api.hip build_cull)
     auto bound_mask = [&](cfloat_p grp, uint32_t b0) -> uint32_t { return bound_mask1(grp, b0 >= S.cflat_lo); };
+    if (wl != nullptr) {  // the grid's blocks (all in the flat section), in list order
+        for (; b < wn; ++b) {
+            const uint32_t bb = S.cflat_lo + (uint32_t)__builtin_amdgcn_readfirstlane((int)wl[b]);
+            if (step(Flat(), bb)) return b + 1u;
+        }
+        return wn;
+    }
     // Three levels above the blocks: a group bound covers the 64 spheres of 8
     // blocks, a super bound the 512 of 8 groups; the super bounds are tested 8
     // at a time (4,096 spheres), then, for each passing super-group, its 8
     // group bounds, for each passing group its 8 block bounds, then the
     // passing blocks' spheres. A resumed scan (b inside a range) masks off
     // the super-groups, groups and blocks before b.
-    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u, nhg = (nsg + 7u) / 8u;
+    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u, nhg = (nsg + 7u) / 8u;  // (nblk: the end)
     for (uint32_t hg = b >> 9; hg < nhg; ++hg) {
         uint32_t m3 = first_bits(nsg - 8u * hg);
         if (RTX_CULL_LEVELS >= 3) m3 &= bound_mask((cfloat_p)S.cbnd3 + 32u * hg, 512u * hg);
@@ -938,8 +950,74 @@ __device__ __forceinline__ HalfTest half_test_stretched(f3 o, f3 d, float thr_bs
     const float as = fmaf(d.z, d.z, fmaf(dys, dys, d.x * d.x));
     return half_test_setup(o.x, kCullSy * o.y, o.z, d.x, dys, d.z, as, thr_bs, t_min);
 }
+// The block-list grid of a large scene's flat layer (rtx_grid.h; DESIGN.md
+// §3f). Each wave keeps an LDS workspace (KScene::cgrid_ws words): [0] the
+// list's length, [1] spare, [2, 2 + bw) a bitmap over the flat section's
+// blocks, then the list (kGridListCap u16 block ids). grid_union: every lane
+// that reaches hit_world walks its ray's slab stretch (the far cut at its best
+// root so far: the non-flat part of the scene is resolved first), and each
+// block its cells name is set in the bitmap and, the first time, appended to
+// the list (LDS atomics). Returns the list's length, or ~0u when some lane
+// gave up (an unsafe ray, too long a walk, a full cell) or the list
+// overflowed: the wave then takes the culled scan over the whole section.
+__device__ __forceinline__ uint32_t grid_union(const KScene &S, uint32_t *ws, f3 o, f3 d, float a, float best,
+                                               bool safe) {
+    const LayerGrid G = *S.cgrid;  // wave-uniform: scalar loads
+    const uint2 *cells = reinterpret_cast<const uint2 *>(S.cgrid + 1);  // kGridListSlots u16 per cell
+    uint32_t *bmp = ws + 2;
+    uint16_t *lst = reinterpret_cast<uint16_t *>(ws + 2 + (G.nblk + 31u) / 32u);
+    auto mark = [&](uint32_t b) {
+        const uint32_t bit = 1u << (b & 31u);
+        const uint32_t old = __hip_atomic_fetch_or(bmp + (b >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((old & bit) == 0u) {
+            const uint32_t i = __hip_atomic_fetch_add(ws, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (i < kGridListCap) lst[i] = (uint16_t)b;
+        }
+    };
+    const float ts = fmaf(G.far_m, __builtin_amdgcn_rsqf(a), best);  // the far cut (+inf: none yet)
+    const bool ok = safe && grid_walk(G, kGridMaxStepsLarge, o.x, o.y, o.z, d.x, d.y, d.z, ts, [&](uint32_t k) {
+                        const uint2 c = cells[k];
+                        if ((c.x & 0xffffu) == kGridFull) return false;
+                        const uint32_t q[4] = {c.x & 0xffffu, c.x >> 16, c.y & 0xffffu, c.y >> 16};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (q[j] != kGridNone) mark(q[j]);
+                        return true;
+                    });
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    return (__ballot(!ok) != 0ull || n > kGridListCap) ? ~0u : n;
+}
+// After the scan: the bitmap back to zero (the listed blocks' words, or every
+// word after an overflow) and the length to 0, by the wave's active lanes.
+__device__ __forceinline__ void grid_clear(const KScene &S, uint32_t *ws) {
+    const uint32_t bw = (S.cgrid_ws - 2u - kGridListCap / 2u);
+    uint32_t *bmp = ws + 2;
+    const uint16_t *lst = reinterpret_cast<const uint16_t *>(ws + 2 + bw);
+    const uint64_t ex = __ballot(1);
+    const uint32_t na = (uint32_t)__popcll(ex);
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u));
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[0]);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (n <= kGridListCap) {
+        for (uint32_t j = r; j < n; j += na) bmp[lst[j] >> 5] = 0u;
+    } else {
+        for (uint32_t j = r; j < bw; j += na) bmp[j] = 0u;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (r == 0u) ws[0] = 0u;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// Zero every wave's workspace (all threads of the block; the caller synchronises).
+__device__ __forceinline__ void grid_ws_zero(const KScene &S, uint32_t *ws0, uint32_t nthreads) {
+    for (uint32_t i = threadIdx.x; i < (nthreads / 64u) * S.cgrid_ws; i += nthreads) ws0[i] = 0u;
+}
+
+// gws: the wave's block-list grid workspace (NULL or a scene without the grid:
+// the culled scan over the whole layout).
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
-                                                float &best, uint32_t *list) {
+                                                float &best, uint32_t *list, uint32_t *gws = nullptr) {
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const LineTest Ts = line_test_stretched(S, o, d);
     const HalfTest H = half_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, T.thr * kCullThrScale, t_min);
@@ -950,14 +1028,33 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     const uint32_t nblk = S.n_cpad / 8u;
     auto ld = [&S](uint32_t p) { return S.ccen[p]; };
     auto gi = [&S](uint32_t p) { return S.cperm[p]; };
-    uint32_t b = 0;
-    do {
-        uint32_t cnt;
-        b = scan_culled(S, b, T, Ts, H, Hs, list, cnt);
+    auto resolve = [&](uint32_t cnt) {
         ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
                                                               idx, cand_of<true>(), gi) &&
              ok;
-    } while (b < nblk);
+    };
+    // the grid (RTX_GRID): the non-flat part first, the flat section by the wave's walks
+    const bool grid = RTX_GRID && gws != nullptr && S.cgrid != nullptr && S.cflat_lo < nblk;
+    const uint32_t end1 = grid ? S.cflat_lo : nblk;
+    uint32_t b = 0;
+    while (b < end1) {
+        uint32_t cnt;
+        b = scan_culled(S, b, end1, T, Ts, H, Hs, list, cnt);
+        resolve(cnt);
+    }
+    if (grid) {
+        const uint32_t wn = grid_union(S, gws, o, d, a, best, T.thr != -__uint_as_float(0x7f800000u));
+        const uint16_t *wl = reinterpret_cast<const uint16_t *>(gws + S.cgrid_ws - kGridListCap / 2u);
+        uint32_t k = wn == ~0u ? S.cflat_lo : 0u;
+        const uint32_t kend = wn == ~0u ? nblk : wn;
+        while (k < kend) {
+            uint32_t cnt;
+            k = wn == ~0u ? scan_culled(S, k, nblk, T, Ts, H, Hs, list, cnt)
+                          : scan_culled(S, k, nblk, T, Ts, H, Hs, list, cnt, wl, wn);
+            resolve(cnt);
+        }
+        grid_clear(S, gws);
+    }
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
@@ -972,9 +1069,6 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
 // through one LDS word per wave, the list's spare row at the wave's first two
 // lanes (`spare`: the list's row `cap`, never a list entry). A lane outside
 // the prefilter's safe range marks every block.
-#ifndef RTX_GRID  // A/B build: 0 = every block of the flat run is scanned
-#define RTX_GRID 1
-#endif
 __device__ __forceinline__ uint64_t grid_wave_mask(const KScene &S, f3 o, f3 d, const LineTest &T, uint32_t *spare) {
     const LayerGrid G = *S.grid;  // wave-uniform: scalar loads
     const uint64_t *gc = reinterpret_cast<const uint64_t *>(S.grid + 1);
@@ -2442,6 +2536,10 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
     const float *pf_tile = kPF && (RTX_PF_LDS || RTX_PF_RING) ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
+    // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
+    uint32_t *gws0 = kCulled && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
+    uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
+    if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     // promotion: the block's first wave to go idle serves the queue, the others leave
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
@@ -2568,7 +2666,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
         if (kCulled) {  // large scenes: the culled scan (block bounds first, scan_culled)
             if (L.active) {
                 float best = __uint_as_float(0x7f800000u);
-                const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
+                const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws);
                 D.section(1);
                 promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
             }
@@ -3092,6 +3190,11 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
+    // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
+    uint32_t *gws0 = kCulled && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + kPsStateBytes)
+                                              : nullptr;
+    uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
+    if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     const SphGlobal sg = sph_global(P.scene);
     const uint32_t lane = threadIdx.x & 63u;
     if (lane < kPsSlots * 4) st[lane] = 0u;
@@ -3164,7 +3267,7 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
-            hit = kCulled ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list)
+            hit = kCulled ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws)
                   : sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                     L.inv_a, kTMin, best, list)
                             : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -3277,6 +3380,12 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
                                                             float t_max, uint32_t start, float *out) {
     __shared__ uint32_t list[list_bytes<true>() > kListBytes ? list_bytes<true>() / sizeof(uint32_t)
                                                              : kListBytes / sizeof(uint32_t)];
+    // the block-list grid's per-wave workspace (dynamic: KScene::cgrid_ws words per wave)
+    extern __shared__ __attribute__((aligned(16))) uint32_t d_gws[];
+    if (S.cgrid) {
+        grid_ws_zero(S, d_gws, kRB);
+        __syncthreads();
+    }
     const uint32_t i = blockIdx.x * kRB + threadIdx.x;
     if (i >= nrays) return;
     const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
@@ -3286,7 +3395,8 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     float best = t_max;
     const int idx =
         min((start == kDebugCulled && S.cpre)
-                ? hit_world_culled(S, o, d, a, inv_a, t_min, best, list)
+                ? hit_world_culled(S, o, d, a, inv_a, t_min, best, list,
+                                   S.cgrid ? d_gws + (threadIdx.x / 64u) * S.cgrid_ws : nullptr)
             : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
                                    : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
@@ -3468,7 +3578,8 @@ static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t s
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() + 16 + (use_lin(s) ? kPfLdsBytes : 0u) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
-           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
+           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0) +
+           (use_pf(s) && s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0);  // the grid's workspaces
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
@@ -3493,7 +3604,8 @@ constexpr uint32_t kPsItems = RTX_PS_ITEMS;
 constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
-           (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
+           (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0) +
+           (use_pf(s) && s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0);  // the grid's workspaces
 }
 static const void *ps_fn(const KScene &s) {
     return !use_pf(s) ? (const void *)k_render_ps<false>
@@ -3724,7 +3836,8 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
                                s, rays, nrays, t_min, t_max, q, out);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
+    const size_t glds = s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0;
+    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), glds, stream, s,
                        rays, nrays, t_min, t_max, start_block, out);
     return hipGetLastError();
 }

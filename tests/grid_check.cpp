@@ -37,8 +37,10 @@ static void unit(double v[3]) {
     v[0] /= n, v[1] /= n, v[2] /= n;
 }
 
-// hit_world32's acceptance of one sphere (best = +inf): a root >= t_min.
-static bool ref_accepts(const float o[3], const float d[3], const float *c, float a, float t_min) {
+// hit_world32's acceptance of one sphere (best = +inf): a root >= t_min;
+// *root receives it.
+static bool ref_accepts(const float o[3], const float d[3], const float *c, float a, float t_min,
+                        float *root = nullptr) {
     const float negr2 = -(c[3] * c[3]);
     const float ocx = o[0] - c[0], ocy = o[1] - c[1], ocz = o[2] - c[2];
     const float hb = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
@@ -47,15 +49,20 @@ static bool ref_accepts(const float o[3], const float d[3], const float *c, floa
     if (disc < 0.0f) return false;
     const float inv_a = 1.0f / a, sq = std::sqrt(disc);
     const float rn = (-hb - sq) * inv_a;
-    if (!(rn < t_min || INFINITY < rn)) return true;
+    if (!(rn < t_min || INFINITY < rn)) {
+        if (root) *root = rn;
+        return true;
+    }
     const float rf = (-hb + sq) * inv_a;
+    if (root) *root = rf;
     return !(rf < t_min || INFINITY < rf);
 }
 
 struct Layer {
     std::vector<float> s;  // (cx, cy, cz, r)
-    rtx::LayerGrid G;
+    rtx::LayerGrid G, Gb;
     std::vector<unsigned long long> cell;
+    std::vector<uint16_t> slots;  // the block-list grid of the same layer (blocks j / 8)
 };
 
 static bool make_layer(Layer &L, bool rtiow) {
@@ -76,13 +83,33 @@ static bool make_layer(Layer &L, bool rtiow) {
             L.s.insert(L.s.end(), {(float)(ext * sym()), y0, (float)(ext * sym()), (float)(rmax * (0.05 + 0.95 * uni()))});
     }
     const uint32_t n = (uint32_t)(L.s.size() / 4);
-    return rtx::build_layer_grid(L.s.data(), 0u, n, L.G, L.cell);
+    std::vector<uint32_t> blk(n);
+    for (uint32_t j = 0; j < n; ++j) blk[j] = j / 8;
+    return rtx::build_layer_grid(L.s.data(), 0u, n, L.G, L.cell) &&
+           rtx::build_layer_grid_blocks(L.s.data(), blk.data(), n, 1u << 20, L.Gb, L.slots);
+}
+
+// The block-list grid's walk as the kernel runs it: the blocks of the cells
+// visited (as a 64-bit mask here: blocks j / 8 < 64), ~0 when it gives up or
+// meets a full cell.
+static uint64_t list_mask(const Layer &L, const float o[3], const float d[3], float t_stop) {
+    uint64_t m = 0ull;
+    const bool done = rtx::grid_walk(L.Gb, 4096u, o[0], o[1], o[2], d[0], d[1], d[2], t_stop, [&](uint32_t k) {
+        const uint16_t *s = &L.slots[(size_t)k * rtx::kGridListSlots];
+        if (s[0] == rtx::kGridFull) return false;
+        for (uint32_t q = 0; q < rtx::kGridListSlots; ++q)
+            if (s[q] != rtx::kGridNone) m |= 1ull << s[q];
+        return true;
+    });
+    return done ? m : ~0ull;
 }
 
 int main(int argc, char **argv) {
     const long nlayers = argc > 1 ? atol(argv[1]) : 300;
     const long nrays = argc > 2 ? atol(argv[2]) : 4000;
     long rays = 0, applied = 0, all = 0, accepted = 0, missed = 0, layers = 0, nogrid = 0;
+    long far_checked = 0, far_missed = 0, list_all = 0, list_missed = 0;
+    double far_bits = 0.0;
     double bits = 0.0;
     for (long li = 0; li < nlayers; ++li) {
         Layer L;
@@ -147,9 +174,17 @@ int main(int argc, char **argv) {
                 continue;
             }
             bits += (double)__builtin_popcountll(m);
+            std::vector<float> roots(n, INFINITY);
+            float win = INFINITY;
+            const uint64_t ml = list_mask(L, of, df, INFINITY);
+            if (ml == ~0ull) ++list_all;
             for (uint32_t i = 0; i < n; ++i) {
                 const float *ci = &L.s[4 * (size_t)i];
-                if (!ref_accepts(of, df, ci, a, 0.0f) && !ref_accepts(of, df, ci, a, 1e-3f)) continue;
+                const bool a0 = ref_accepts(of, df, ci, a, 0.0f);
+                const bool a1 = ref_accepts(of, df, ci, a, 1e-3f, &roots[i]);
+                if (!a1) roots[i] = INFINITY;
+                win = fminf(win, roots[i]);
+                if (!a0 && !a1) continue;
                 ++accepted;
                 if (!((m >> (i / 8)) & 1ull)) {
                     if (missed < 5)
@@ -157,12 +192,39 @@ int main(int argc, char **argv) {
                                 ci[0], ci[1], ci[2], ci[3], of[0], of[1], of[2], df[0], df[1], df[2]);
                     ++missed;
                 }
+                if (!((ml >> (i / 8)) & 1ull)) ++list_missed;
+            }
+            // the far cut (t_min 1e-3, the render's): B at the winner's own root
+            // (a tie goes to the later sphere: every root <= B must be scanned),
+            // and at a random fraction of it, t_stop = B + far_m / |d| in fp32
+            if (win < INFINITY) {
+                const float inv_len = 1.0f / std::sqrt(a);
+                for (int rep = 0; rep < 2; ++rep) {
+                    const float B = rep == 0 ? win : win * (float)(0.5 + uni());
+                    const float ts = fmaf(L.G.far_m, inv_len, B);
+                    const uint64_t mf = rtx::grid_mask(L.G, cellf, of[0], of[1], of[2], df[0], df[1], df[2], ts);
+                    const uint64_t mlf = list_mask(L, of, df, fmaf(L.Gb.far_m, inv_len, B));
+                    far_bits += (double)__builtin_popcountll(mf);
+                    for (uint32_t i = 0; i < n; ++i) {
+                        if (!(roots[i] <= B)) continue;
+                        ++far_checked;
+                        const bool hit_m = (mf >> (i / 8)) & 1ull, hit_l = (mlf >> (i / 8)) & 1ull;
+                        if (!hit_m || !hit_l) {
+                            if (far_missed < 5)
+                                fprintf(stderr, "far miss: sphere %u root %.9g B %.9g o (%.9g %.9g %.9g) d (%.9g %.9g %.9g)\n",
+                                        i, roots[i], B, of[0], of[1], of[2], df[0], df[1], df[2]);
+                            ++far_missed;
+                        }
+                    }
+                }
             }
         }
     }
     const long masked = applied - all;
     printf("{\"layers\": %ld, \"layers_without_grid\": %ld, \"rays\": %ld, \"grid_applied\": %ld, "
-           "\"every_block\": %ld, \"accepted_spheres\": %ld, \"missed\": %ld, \"mean_blocks_marked\": %.3f}\n",
-           layers, nogrid, rays, applied, all, accepted, missed, masked ? bits / (double)masked : 0.0);
-    return missed == 0 ? 0 : 1;
+           "\"every_block\": %ld, \"accepted_spheres\": %ld, \"missed\": %ld, \"mean_blocks_marked\": %.3f, "
+           "\"far_checked\": %ld, \"far_missed\": %ld, \"list_every_block\": %ld, \"list_missed\": %ld}\n",
+           layers, nogrid, rays, applied, all, accepted, missed, masked ? bits / (double)masked : 0.0, far_checked,
+           far_missed, list_all, list_missed);
+    return missed == 0 && far_missed == 0 && list_missed == 0 ? 0 : 1;
 }

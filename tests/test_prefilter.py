@@ -70,13 +70,17 @@ def test_layer_grid_never_skips_an_accepted_sphere(tmp_path):
     assert out.returncode == 0 and rep["missed"] == 0, out.stderr
     assert rep["accepted_spheres"] > 3_000_000 and rep["grid_applied"] > 900_000, rep
     assert rep["every_block"] < 0.01 * rep["grid_applied"], rep  # the walk rarely gives up
+    # the far cut (the walk stops far_m / |d| past the best root so far: the
+    # winner's own root, ties included) and the block-list grid (large scenes)
+    assert rep["far_missed"] == 0 and rep["far_checked"] > 500_000, rep
+    assert rep["list_missed"] == 0 and rep["list_every_block"] < 0.01 * rep["grid_applied"], rep
     # sensitivity: the same checker over a grid without the margins misses
     bad = tmp_path / "bad" / "raytrace-we-gpu_amd" / "csrc"
     bad.mkdir(parents=True)
     src = open(os.path.join(ROOT, "raytrace-we-gpu_amd", "csrc", "rtx_grid.h")).read()
     src = src.replace("constexpr double kGridFatCells = 1.0 / 256.0;", "constexpr double kGridFatCells = 0.0;")
     src = src.replace(" + 27.0 * u * c2 + B) * (1.0 + 4.0 * u) * (1.0 + 1e-12)", ") * (1.0 - 1e-7)")
-    assert src.count("(1.0 - 1e-7)") == 2
+    assert src.count("(1.0 - 1e-7)") == 1
     (bad / "rtx_grid.h").write_text(src)
     (bad / "rtx_prefilter.h").write_text(open(os.path.join(ROOT, "raytrace-we-gpu_amd", "csrc",
                                                            "rtx_prefilter.h")).read())
