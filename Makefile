@@ -18,7 +18,14 @@ HDRS      := include/rtx.h $(SRC)/rtx_internal.h $(SRC)/rtx_device_math.h $(SRC)
 LIBSRCS   := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/*.cpp)) include/rtx.h
 SRC_SHA   := $(shell python3 tools/src_sha.py)
 
-all: $(LIB) $(CLI) oracle $(LIBDIR)/variants/librtx_stress.so
+UBENCH    := tools/ubench_issue
+
+all: $(LIB) $(CLI) oracle $(LIBDIR)/variants/librtx_stress.so $(UBENCH)
+
+# VALU issue cost per instruction class in the chip's own cycles (bench.py's
+# issue ceiling, tools/issue_probe.py)
+$(UBENCH): tools/ubench_issue.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 $(LIBDIR)/%.o: $(SRC)/%.hip $(HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -266,39 +266,59 @@ def pmc_valu(args, n_cu, launch_ms, rng=None):
             "counters": v, "stall_counters": w, "cus": n_cu}
 
 
-SCAN_REPS = 200
+UBENCH = os.path.join(ROOT, "tools", "ubench_issue")
 
 
-def issue_ceiling(args, ctx, executed, n_cu):
-    """The VALU issue rate hit_world's own instruction mix sustains at the
-    render's occupancy: rtx_debug_scan_rate runs the
-    render's lane-mode hit_world (prefiltered scan + resolve) and nothing
-    else on a full-occupancy grid of the render's shape; one rocprofv3 pass
-    over that launch gives its VALU instructions per SIMD-cycle. The render's
-    rate over the same measure says how close the whole kernel (scan, resolve,
-    shading, scheduling) runs to that ceiling. Small scenes (<= 640 spheres)."""
+def issue_ceiling(args, executed, n_cu):
+    """The VALU issue ceiling at the render's occupancy,
+    in the chip's own cycles: tools/ubench_issue issues independent
+    v_fma_f32 (and v_pk_fma_f32, integer, transcendental) streams at 1, 2, 5
+    and 8 waves per SIMD, one rocprofv3 pass gives SQ_INSTS_VALU and
+    GRBM_GUI_ACTIVE per kernel; cycles per VALU instruction = 4 * CUs *
+    GRBM_GUI_ACTIVE/8 / SQ_INSTS_VALU (the real clock, DVFS included). No
+    instruction class of the render's mix issues faster than an independent
+    v_fma_f32 stream at the same occupancy, so the fma stream at the render's
+    resident waves (rounded up: the generous side) is a rate the render
+    cannot beat; render_frac_of_ceiling = its cycles / the render's."""
     if not executed or "counters" not in executed:
         return {"skipped": "needs the N=1 PMC passes"}
-    ms, wave_segs = ctx.debug_scan_rate(SCAN_REPS)  # (a warm run; the profiled one is the --probe child's)
+    if not os.path.exists(UBENCH):
+        return {"skipped": f"{os.path.relpath(UBENCH, ROOT)} not built (make)"}
+    exe = shutil.which("rocprofv3")
+    out = tempfile.mkdtemp(prefix="rtx_ubench_")
     try:
-        v = _pmc_pass(args, ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"], "scan",
-                      extra=["--probe-scan", str(SCAN_REPS)])
-    except RuntimeError as e:
-        return {"skipped": str(e)}
+        cmd = [exe, "--pmc", "SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "--output-format", "csv", "-d", out,
+               "-o", "ub", "--", UBENCH, "4000"]
+        subprocess.run(cmd, check=True, capture_output=True, timeout=240)
+        disp = {}
+        for path in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
+            for row in csv.DictReader(open(path)):
+                d = disp.setdefault(int(row["Dispatch_Id"]), {"kernel": row["Kernel_Name"]})
+                d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    except (subprocess.SubprocessError, OSError, KeyError, ValueError) as e:
+        return {"skipped": f"ubench pass failed: {type(e).__name__}"}
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
     simds = 4 * n_cu
-    probe_ipc = v["SQ_INSTS_VALU"] / (simds * v["GRBM_GUI_ACTIVE"] / 8.0)
+    rates = {}
+    for i in sorted(disp):  # the second launch of each kernel overwrites the first
+        m = re.search(r"k_(\w+?)<(\d+)>", disp[i]["kernel"])
+        if m and disp[i].get("SQ_INSTS_VALU"):
+            rates[f"{m.group(1)}@{m.group(2)}"] = round(
+                simds * disp[i]["GRBM_GUI_ACTIVE"] / 8.0 / disp[i]["SQ_INSTS_VALU"], 3)
     rc = executed["counters"]
-    render_ipc = rc["SQ_INSTS_VALU"] / (simds * rc["GRBM_GUI_ACTIVE"] / 8.0)
-    return {"probe": "rtx_debug_scan_rate: the render's lane-mode hit_world alone, full occupancy, "
-                     f"{SCAN_REPS} reps of one primary ray per lane",
-            "probe_ms": round(ms, 3), "probe_wave_segments": wave_segs,
-            "probe_valu_per_wave_segment": round(v["SQ_INSTS_VALU"] / max(1, wave_segs), 1),
-            "probe_valu_per_simd_cycle": round(probe_ipc, 4),
-            "probe_cycles_per_valu": round(1.0 / probe_ipc, 3) if probe_ipc else None,
-            "render_valu_per_simd_cycle": round(render_ipc, 4),
-            "render_cycles_per_valu": round(1.0 / render_ipc, 3) if render_ipc else None,
-            "render_frac_of_ceiling": round(render_ipc / probe_ipc, 4) if probe_ipc else None,
-            "counters": {k: v[k] for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE")}}
+    render_cpv = simds * rc["GRBM_GUI_ACTIVE"] / 8.0 / rc["SQ_INSTS_VALU"]
+    occ = executed.get("wave_cycles", {}).get("resident_waves_per_simd") or 5.0
+    fma = {int(k.split("@")[1]): v for k, v in rates.items() if k.startswith("fma@")}
+    w = min([x for x in fma if x >= occ] or [max(fma)]) if fma else None
+    ceil_cpv = fma.get(w) if w else None
+    return {"probe": "tools/ubench_issue: independent VALU streams per class and occupancy, one rocprofv3 pass; "
+                     "cycles per VALU instruction in the chip's own clock (GRBM_GUI_ACTIVE)",
+            "cycles_per_valu_by_class": rates,
+            "render_resident_waves_per_simd": occ, "ceiling_class": f"fma@{w}" if w else None,
+            "ceiling_cycles_per_valu": ceil_cpv,
+            "render_cycles_per_valu": round(render_cpv, 3),
+            "render_frac_of_ceiling": round(ceil_cpv / render_cpv, 4) if ceil_cpv else None}
 
 
 def roofline_of(executed, launch_ms, tests_per_launch):
@@ -730,8 +750,7 @@ def main():
         if args.pmc == "auto" and R == 1:
             traffic, pmc_note = pmc_traffic(args)
             executed = pmc_valu(args, n_cu, launch_ms)
-            if world.count <= 640 and args.rng == "chain":
-                ceiling = issue_ceiling(args, ctx, executed, n_cu)
+            ceiling = issue_ceiling(args, executed, n_cu)
         host_img = image.cpu().numpy()
         cpu, parity = (None, None)
         if R == 1 and args.cpu_seconds > 0:

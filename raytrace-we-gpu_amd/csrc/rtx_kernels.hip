@@ -1014,8 +1014,11 @@ __device__ __forceinline__ void grid_ws_zero(const KScene &S, uint32_t *ws0, uin
     for (uint32_t i = threadIdx.x; i < (nthreads / 64u) * S.cgrid_ws; i += nthreads) ws0[i] = 0u;
 }
 
-// gws: the wave's block-list grid workspace (NULL or a scene without the grid:
-// the culled scan over the whole layout).
+// kGrid (its own kernel instances: the grid's code costs the plain culled
+// kernels registers they spill, R10e): gws is the wave's block-list grid
+// workspace (NULL or a scene without the grid: the culled scan over the
+// whole layout).
+template <bool kGrid = false>
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
                                                 float &best, uint32_t *list, uint32_t *gws = nullptr) {
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
@@ -1034,7 +1037,7 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
              ok;
     };
     // the grid (RTX_GRID): the non-flat part first, the flat section by the wave's walks
-    const bool grid = RTX_GRID && gws != nullptr && S.cgrid != nullptr && S.cflat_lo < nblk;
+    const bool grid = kGrid && RTX_GRID && gws != nullptr && S.cgrid != nullptr && S.cflat_lo < nblk;
     const uint32_t end1 = grid ? S.cflat_lo : nblk;
     uint32_t b = 0;
     while (b < end1) {
@@ -1042,7 +1045,8 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
         b = scan_culled(S, b, end1, T, Ts, H, Hs, list, cnt);
         resolve(cnt);
     }
-    if (grid) {
+    if constexpr (kGrid) {
+      if (grid) {
         const uint32_t wn = grid_union(S, gws, o, d, a, best, T.thr != -__uint_as_float(0x7f800000u));
         const uint16_t *wl = reinterpret_cast<const uint16_t *>(gws + S.cgrid_ws - kGridListCap / 2u);
         uint32_t k = wn == ~0u ? S.cflat_lo : 0u;
@@ -1054,6 +1058,7 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
             resolve(cnt);
         }
         grid_clear(S, gws);
+      }
     }
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
@@ -1103,7 +1108,7 @@ __device__ __forceinline__ uint64_t grid_wave_mask(const KScene &S, f3 o, f3 d, 
 // waves that trail it, instead of every wave missing on every block.
 // start (no pack word): the block to start at (rtx_debug_hit_world_from),
 // wave-uniform.
-template <bool kPF, typename Ld, bool kTile = false>
+template <bool kPF, typename Ld, bool kTile = false, bool kGridOk = true>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
                                                 float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
                                                 uint32_t start = 0, const float *lds_pr = nullptr,
@@ -1117,7 +1122,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     }
     // the layer grid (small scenes, rtx_grid.h): the flat run's blocks some lane of the wave needs
     uint64_t gm = ~0ull;
-    if constexpr (!kPF) {
+    if constexpr (!kPF && kGridOk) {
         if (RTX_GRID && S.grid != nullptr) gm = grid_wave_mask(S, o, d, T, list + cand_of<kPF>() * kRB);
     }
     const float best0 = best;
@@ -1148,13 +1153,15 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     }
     return idx;
 }
-template <bool kPF>
+// kGridOk false: no layer grid (a kernel that has no other use for its code:
+// the large-scene kernels' rare exact fallback)
+template <bool kPF, bool kGridOk = true>
 __device__ __forceinline__ int hit_world_pre(const KScene &S, f3 o, f3 d, float a, float inv_a,
                                              float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
                                              uint32_t start = 0) {
     const float4 *__restrict__ cen = S.cen;
-    return hit_world_pre_ld<kPF>(S, [cen](uint32_t i) { return cen[i]; }, o, d, a, inv_a, t_min, best, list, pack,
-                                 start);
+    auto ld = [cen](uint32_t i) { return cen[i]; };
+    return hit_world_pre_ld<kPF, decltype(ld), false, kGridOk>(S, ld, o, d, a, inv_a, t_min, best, list, pack, start);
 }
 
 // ---- group-cooperative hit_world (frame tail, heavy tiers) -----------------
@@ -2191,9 +2198,13 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // material fetch are then as cheap as in a whole-wave-only kernel (a
 // runtime lg cost the one-pixel-per-wave case 2.0 -> 2.5 us per segment,
 // profiles/R6f_pixel_timeline_r8.jsonl).
+// glist (a wave's LDS for the layer grid: 64 bytes per group; NULL: none):
+// the group scans only its ray's blocks — the blocks outside the scene's flat
+// run and the flat-run blocks its slab walk marks (rtx_grid.h grid_mask) —
+// listed in index order, 4 sphere pairs per block (scenes of up to 64 blocks).
 template <uint32_t kLg, typename Src>
 __device__ __forceinline__ void trace_group_segment(const KParams &P, const Frame &F, const Src &src, Lane &W,
-                                                    bool &ended) {
+                                                    bool &ended, uint8_t *glist = nullptr) {
     constexpr uint32_t lg = kLg;
     const KScene &S = P.scene;
     const uint32_t lane = threadIdx.x & 63u;
@@ -2203,7 +2214,38 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const int last = (int)S.n - 1;
     const ScatterSpec sp = scatter_spec(W.seed);
     LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
-    if (lg < 6u && !W.active) {  // a group without a pixel: nothing is flagged (a whole wave is always active)
+    const bool idle = lg < 6u && !W.active;  // a group without a pixel: nothing is flagged (a whole wave is always active)
+    // the layer grid: this group's blocks, in order, into its glist (the walk is
+    // the same in every lane of the group: the same ray)
+    uint8_t *gl = glist ? glist + 64u * (lane >> lg) : nullptr;
+    uint32_t gcnt = 0;
+    if (gl != nullptr) {
+        const uint32_t nblk = S.n_pad / 8u;
+        const uint64_t all = nblk >= 64u ? ~0ull : (1ull << nblk) - 1ull;
+        const uint32_t fl = S.flat_hi - S.flat_lo;
+        const uint64_t run = (fl >= 64u ? ~0ull : (1ull << fl) - 1ull) << S.flat_lo;
+        uint64_t fm = 0ull;
+        if (!idle) {
+            const LayerGrid G = *S.grid;
+            const uint64_t *gc = reinterpret_cast<const uint64_t *>(S.grid + 1);
+            fm = T.thr == -inf ? ~0ull
+                               : grid_mask(G, [gc](uint32_t c) { return gc[c]; }, W.o.x, W.o.y, W.o.z, W.d.x, W.d.y,
+                                           W.d.z);
+        }
+        const uint64_t cm = idle ? 0ull : (all & ~run) | ((fm << S.flat_lo) & run);
+        constexpr uint32_t kBpl = 64u >> lg;  // bits per lane of the group
+#pragma unroll
+        for (uint32_t j = 0; j < kBpl; ++j) {
+            const uint32_t bit = k * kBpl + j;
+            if ((cm >> bit) & 1ull) gl[__popcll(cm & ((1ull << bit) - 1ull))] = (uint8_t)bit;
+        }
+        gcnt = (uint32_t)__popcll(cm);
+        // the lists are read by other lanes of the group: LDS keeps one wave's
+        // operations in order; the compiler must too
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    }
+    if (idle) {
         T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
         T.thr = inf;
     }
@@ -2211,7 +2253,20 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
     uint64_t key = hit_key(inf, -1);
     bool ok = true;
-    const uint32_t nsteps = src.npairs >> lg;  // SphLds: npairs is a multiple of 64
+    // the steps: every pair (SphLds: npairs is a multiple of 64), or, with the
+    // grid, the most any group of the wave needs (4 pairs per listed block)
+    const uint32_t npairs_g = 4u * gcnt;
+    const uint32_t nsteps = gl ? (group_reduce_u32<true>(npairs_g, 6u) + g - 1u) >> lg : src.npairs >> lg;
+    // step st's pair of this lane (valid: it has one)
+    auto pair_of = [&](uint32_t st, bool &valid) -> uint32_t {
+        if (gl == nullptr) {
+            valid = true;
+            return (st << lg) + k;
+        }
+        const uint32_t pos = (st << lg) + k;
+        valid = pos < npairs_g;
+        return valid ? 4u * (uint32_t)gl[pos >> 2] + (pos & 3u) : 0u;
+    };
 #pragma unroll 1
     for (uint32_t s0 = 0; s0 < nsteps; s0 += kGfSteps) {
         // the group coop's scan and resolve (hit_world_groups)
@@ -2219,10 +2274,12 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
         const uint32_t s1 = min(s0 + kGfSteps, nsteps);
         auto step = [&](uint32_t st) {
             f2v cx, cy, cz, R;
-            src.pair((st << lg) + k, cx, cy, cz, R);
+            bool valid;
+            src.pair(pair_of(st, valid), cx, cy, cz, R);
             const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
             const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
-            const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
+            f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
+            if (!valid) q = f2v{-inf, -inf};  // no pair: not flagged
             im = (im << 1) | (__float_as_uint(q.y) >> 31);
             im = (im << 1) | (__float_as_uint(q.x) >> 31);
         };
@@ -2239,7 +2296,8 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
             const bool live = fm != 0u;
             const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
             fm &= fm - 1u;
-            const uint32_t p = ((s1 - 1u - (bit >> 1)) << lg) + k;
+            bool valid;
+            const uint32_t p = pair_of(s1 - 1u - (bit >> 1), valid);
             const uint32_t j = 2u * p + (bit & 1u);
             resolve_one(src.sphere(j), (int)j, live, W.o, W.d, W.a, W.inv_a, kTMin, key, ok);
         }
@@ -2520,9 +2578,10 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
-template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false>
+template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false, bool kGrid = false>
 __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
+    constexpr bool kCGrid = kCulled && kGrid;            // ... with the block-list layer grid
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][coop LDS copy of the spheres]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -2537,7 +2596,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
     const float *pf_tile = kPF && (RTX_PF_LDS || RTX_PF_RING) ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
     // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
-    uint32_t *gws0 = kCulled && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
+    uint32_t *gws0 = kCGrid && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
     uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
     if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     // promotion: the block's first wave to go idle serves the queue, the others leave
@@ -2637,7 +2696,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
             if (L.active) {
                 if (my_seq) {  // (rare: the plain scan, so the kPF ping-pong's SGPRs stay out of this kernel)
                     my_best = __uint_as_float(0x7f800000u);
-                    my_hit = hit_world_pre<false>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
+                    my_hit = hit_world_pre<false, !kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, my_best, list);
                 }
                 // the tail's pixels may be promoted (tier-1 waves already
                 // trace one ray with every lane; promoting tier-2 pixels
@@ -2666,7 +2725,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
         if (kCulled) {  // large scenes: the culled scan (block bounds first, scan_culled)
             if (L.active) {
                 float best = __uint_as_float(0x7f800000u);
-                const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws);
+                const int hit = hit_world_culled<kCGrid>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws);
                 D.section(1);
                 promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
             }
@@ -2815,9 +2874,16 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
 // copy, took LDS the render's blocks needed: at R = 8 (7 k_trace waves per
 // CU) only ~79 % of k_render's lanes were resident (profiles/R6r_pixel_timelines.jsonl).
 constexpr uint32_t kTraceThreads = 256;
+constexpr uint32_t kTraceGlistBytes = 8u * 64u;  // per wave: 8 groups' block lists (trace_group_segment)
+__host__ __device__ constexpr uint32_t trace_glist_off(uint32_t n) { return (coop_lds_bytes(n) + 15u) & ~15u; }
 __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem), true, kTraceThreads);
+    // the layer grid's per-group block lists (64 bytes per group, 8 groups per
+    // wave at most), after the scene copy (trace_group_segment)
+    uint8_t *glist = P.scene.grid && P.scene.n_pad <= 512u
+                         ? s_mem + trace_glist_off(P.scene.n) + (threadIdx.x / 64u) * kTraceGlistBytes
+                         : nullptr;
     __syncthreads();
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
@@ -2893,7 +2959,7 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             // is this pixel's critical path)
             uint32_t n = 0;
             do {
-                trace_group_segment<6>(P, F, sl, W, ended);
+                trace_group_segment<6>(P, F, sl, W, ended, glist);
                 ++n;
                 if (P.prom) beat(P, last_beat);
             } while (!ended);
@@ -2901,11 +2967,11 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
         } else {
             if (P.prom) beat(P, last_beat);
             if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 or 8 (rtx_set_schedule)
-                trace_group_segment<5>(P, F, sl, W, ended);
+                trace_group_segment<5>(P, F, sl, W, ended, glist);
             else if (lg == 4u)
-                trace_group_segment<4>(P, F, sl, W, ended);
+                trace_group_segment<4>(P, F, sl, W, ended, glist);
             else  // 8 pixels per wave, 8 lanes each: a third of the issue per pixel-segment of 16-lane groups
-                trace_group_segment<3>(P, F, sl, W, ended);
+                trace_group_segment<3>(P, F, sl, W, ended, glist);
             if (W.active && first) segs++;
         }
         if (ended) {
@@ -3177,9 +3243,10 @@ __device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t
     output_pixel(P, px0 + po, acc);
 }
 
-template <bool kPF, bool kLin = false>
+template <bool kPF, bool kLin = false, bool kGrid = false>
 __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
+    constexpr bool kCGrid = kCulled && kGrid;            // ... with the block-list layer grid
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][batch slots, kPsStateBytes]
     //              [LDS copy of the spheres (n <= kCoopLds)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -3191,8 +3258,8 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
     // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
-    uint32_t *gws0 = kCulled && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + kPsStateBytes)
-                                              : nullptr;
+    uint32_t *gws0 = kCGrid && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + kPsStateBytes)
+                                             : nullptr;
     uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
     if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     const SphGlobal sg = sph_global(P.scene);
@@ -3267,7 +3334,7 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
-            hit = kCulled ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws)
+            hit = kCulled ? hit_world_culled<kCGrid>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws)
                   : sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                     L.inv_a, kTMin, best, list)
                             : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -3395,8 +3462,8 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     float best = t_max;
     const int idx =
         min((start == kDebugCulled && S.cpre)
-                ? hit_world_culled(S, o, d, a, inv_a, t_min, best, list,
-                                   S.cgrid ? d_gws + (threadIdx.x / 64u) * S.cgrid_ws : nullptr)
+                ? hit_world_culled<true>(S, o, d, a, inv_a, t_min, best, list,
+                                         S.cgrid ? d_gws + (threadIdx.x / 64u) * S.cgrid_ws : nullptr)
             : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
                                    : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
@@ -3558,11 +3625,14 @@ static bool use_pf(const KScene &s) { return s.n_pad > kScanPfMin; }
 // every block of every segment (the reference's Hittable_list order of work,
 // with the prefilter), through the per-wave LDS tile in the chain render.
 static bool use_lin(const KScene &s) { return use_pf(s) && s.cpre == nullptr; }
+// the block-list layer grid (culled large scenes uploaded with one): its own instances
+static bool use_cgrid(const KScene &s) { return use_pf(s) && s.cpre != nullptr && s.cgrid != nullptr; }
 template <bool kPersist, bool kCost>
 static const void *render_fn(const KScene &s) {
-    return !use_pf(s) ? (const void *)k_render<kPersist, kCost, false>
-           : use_lin(s) ? (const void *)k_render<kPersist, kCost, true, true>
-                        : (const void *)k_render<kPersist, kCost, true>;
+    return !use_pf(s)     ? (const void *)k_render<kPersist, kCost, false>
+           : use_lin(s)   ? (const void *)k_render<kPersist, kCost, true, true>
+           : use_cgrid(s) ? (const void *)k_render<kPersist, kCost, true, false, true>
+                          : (const void *)k_render<kPersist, kCost, true>;
 }
 template <bool kPersist, bool kCost>
 static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t stream, const KParams &a) {
@@ -3570,6 +3640,8 @@ static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((k_render<kPersist, kCost, false>), dim3(blocks), dim3(kRB), lds, stream, a);
     else if (use_lin(s))
         hipLaunchKernelGGL((k_render<kPersist, kCost, true, true>), dim3(blocks), dim3(kRB), lds, stream, a);
+    else if (use_cgrid(s))
+        hipLaunchKernelGGL((k_render<kPersist, kCost, true, false, true>), dim3(blocks), dim3(kRB), lds, stream, a);
     else
         hipLaunchKernelGGL((k_render<kPersist, kCost, true>), dim3(blocks), dim3(kRB), lds, stream, a);
 }
@@ -3608,8 +3680,10 @@ static size_t ps_lds(const KScene &s) {
            (use_pf(s) && s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0);  // the grid's workspaces
 }
 static const void *ps_fn(const KScene &s) {
-    return !use_pf(s) ? (const void *)k_render_ps<false>
-           : use_lin(s) ? (const void *)k_render_ps<true, true> : (const void *)k_render_ps<true>;
+    return !use_pf(s)     ? (const void *)k_render_ps<false>
+           : use_lin(s)   ? (const void *)k_render_ps<true, true>
+           : use_cgrid(s) ? (const void *)k_render_ps<true, false, true>
+                          : (const void *)k_render_ps<true>;
 }
 static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
 // Every resident wave (an item is a sample, not a pixel: a frame share with
@@ -3644,6 +3718,8 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
         hipLaunchKernelGGL(k_render_ps<false>, dim3(blocks), dim3(kRB), lds, stream, q);
     else if (use_lin(p.scene))
         hipLaunchKernelGGL((k_render_ps<true, true>), dim3(blocks), dim3(kRB), lds, stream, q);
+    else if (use_cgrid(p.scene))
+        hipLaunchKernelGGL((k_render_ps<true, false, true>), dim3(blocks), dim3(kRB), lds, stream, q);
     else
         hipLaunchKernelGGL(k_render_ps<true>, dim3(blocks), dim3(kRB), lds, stream, q);
     return hipGetLastError();
@@ -3789,7 +3865,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     if (trace_waves > 0) {
         q.trace_ext = 1u;
         q.trace_lg = 6u - (uint32_t)__builtin_ctz(max(1u, min(tune.trace_group, 64u)));
-        const size_t tlds = coop_lds_bytes(p.scene.n);
+        const size_t tlds = trace_glist_off(p.scene.n) + (kTraceThreads / 64u) * kTraceGlistBytes;
         e = hipEventRecord(sched.ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(sched.aux, sched.ev_fork, 0);
         if (e != hipSuccess) return e;
