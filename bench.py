@@ -123,7 +123,7 @@ def probe(args):
 def kernel_class(name):
     """The role of one dispatch of an rtx_render_rows launch (rocprof
     Kernel_Name), or None for the HIP runtime's own fills and copies."""
-    m = re.search(r"k_render<(true|false), (true|false), (true|false)(, (true|false))?>", name)
+    m = re.search(r"k_render<(true|false), (true|false), (true|false)(?:, (?:true|false))*>", name)
     if m:
         if m.group(2) == "true":
             return "prepass"

@@ -89,10 +89,6 @@ struct rtx_ctx {
     // layer grid of the flat run (small scenes; rtx_grid.h; none: null):
     // its LayerGrid, then the cells' block masks
     rtx::LayerGrid *d_grid = nullptr;
-    // block-list grid of the culled layout's flat section (large scenes): its
-    // LayerGrid, then kGridListSlots u16 block ids per cell; cgrid_ws: LDS words per wave
-    rtx::LayerGrid *d_cgrid = nullptr;
-    uint32_t cgrid_ws = 0;
     int scan_mode = RTX_SCAN_AUTO;  // rtx_set_scan_mode: applied by rtx_upload_world
     float4 *d_cen = nullptr;
     int *d_mtype = nullptr;
@@ -199,9 +195,6 @@ void free_world(rtx_ctx *c) {
     (void)hipFree(c->d_ccen);
     (void)hipFree(c->d_grid);
     c->d_grid = nullptr;
-    (void)hipFree(c->d_cgrid);
-    c->d_cgrid = nullptr;
-    c->cgrid_ws = 0;
     c->d_cpre = c->d_cbnd = c->d_cbnd2 = c->d_cbnd3 = nullptr;
     c->d_cperm = nullptr;
     c->d_ccen = nullptr;
@@ -238,8 +231,6 @@ rtx::KScene scene_of(const rtx_ctx *c) {
     s.n_cpad = c->n_cpad;
     s.cflat_lo = c->cflat_lo;
     s.grid = c->d_grid;
-    s.cgrid = c->d_cgrid;
-    s.cgrid_ws = c->cgrid_ws;
     return s;
 }
 
@@ -762,22 +753,6 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         c->n_cpad = (uint32_t)cl.perm.size();
         c->cflat_lo = cl.flat_lo;
     }
-    // the large-scene lane mode's block-list grid over the culled layout's flat section
-    rtx::LayerGrid cgrid{};
-    std::vector<uint16_t> cslots;
-    bool has_cgrid = false;
-    if (RTX_GRID_UPLOAD && cull && cl.flat_lo < cl.perm.size() / 8) {
-        std::vector<float> fs;
-        std::vector<uint32_t> fb;
-        for (size_t p = 8 * (size_t)cl.flat_lo; p < cl.perm.size(); ++p) {
-            if (cl.pad[p]) continue;  // padding copies never pass (R = -inf): nothing to find
-            const float *sp = w->spheres + 4 * (size_t)cl.perm[p];
-            fs.insert(fs.end(), {sp[0], sp[1], sp[2], sp[3]});
-            fb.push_back((uint32_t)(p / 8) - cl.flat_lo);
-        }
-        has_cgrid = !fb.empty() && rtx::build_layer_grid_blocks(fs.data(), fb.data(), (uint32_t)fb.size(), 1u << 22,
-                                                                 cgrid, cslots);
-    }
     if (has_grid) {
         static_assert(sizeof(rtx::LayerGrid) % 8 == 0, "the cells follow the LayerGrid, 8-byte aligned");
         std::vector<unsigned long long> buf(sizeof(rtx::LayerGrid) / 8 + gcell.size());
@@ -787,15 +762,6 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
         RTX_HIP(hipMemcpyAsync(c->d_grid, buf.data(), buf.size() * sizeof(unsigned long long), hipMemcpyHostToDevice,
                                c->stream));
         RTX_HIP(hipStreamSynchronize(c->stream));
-    }
-    if (has_cgrid) {
-        std::vector<uint16_t> buf(sizeof(rtx::LayerGrid) / 2 + cslots.size());
-        std::memcpy(buf.data(), &cgrid, sizeof cgrid);
-        std::memcpy(buf.data() + sizeof(rtx::LayerGrid) / 2, cslots.data(), cslots.size() * sizeof(uint16_t));
-        RTX_HIP(hipMalloc(&c->d_cgrid, buf.size() * sizeof(uint16_t)));
-        RTX_HIP(hipMemcpyAsync(c->d_cgrid, buf.data(), buf.size() * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
-        RTX_HIP(hipStreamSynchronize(c->stream));
-        c->cgrid_ws = rtx::grid_ws_words(cgrid.nblk);
     }
     if (c->n != n) c->n_changed = true;
     c->n = n;

@@ -63,15 +63,8 @@ namespace rtx {
 constexpr float kGridOMax = 64.0f;      // rays with |o| above this scan every block
 constexpr double kGridFatCells = 1.0 / 256.0;  // cell-list fattening, in cells
 constexpr double kGridSlabPad = 1e-3;          // slab half-width past rho_max (y units)
-constexpr uint32_t kGridMaxSteps = 48;  // a longer walk (the block-mask grid) scans every block
-constexpr uint32_t kGridMaxCells = 4096;  // the block-mask grid (small scenes)
-constexpr uint32_t kGridListSlots = 4;    // the block-list grid (large scenes): block ids per cell
-constexpr uint16_t kGridNone = 0xffffu;   // ... an empty slot
-constexpr uint16_t kGridFull = 0xfffeu;   // ... the cell needs more blocks than it holds: every block
-constexpr uint32_t kGridListCap = 256;     // blocks a wave's union lists (rtx_kernels.hip grid_union)
-constexpr uint32_t kGridMaxStepsLarge = 96;  // a longer walk (the block-list grid) takes the culled scan
-// LDS words per wave of the block-list grid's union: length, spare, bitmap, list
-RTX_GD constexpr uint32_t grid_ws_words(uint32_t nblk_flat) { return 2u + (nblk_flat + 31u) / 32u + kGridListCap / 2u; }
+constexpr uint32_t kGridMaxSteps = 48;  // a longer walk scans every block
+constexpr uint32_t kGridMaxCells = 4096;  // cells of a grid at most
 
 struct LayerGrid {
     float x0, z0;      // the grid's corner (multiples of h)
@@ -79,12 +72,12 @@ struct LayerGrid {
     float ylo, yhi;    // the slab: y0 -+ (rho_max + kGridSlabPad), rounded outwards
     uint32_t nx, nz;   // cells along x and z; cell (ix, iz) covers [x0 + ix h, x0 + (ix + 1) h] x ...
     float far_m;       // far cut: the walk may stop kGridFar(...) past the best root so far (distance units)
-    uint32_t nblk;     // blocks the cells name (the block-list grid's bitmap size; the mask grid: <= 64)
+    uint32_t nblk;     // blocks the cells' masks name (<= 64)
 };
 
-// The far cut (the block-list grid). A walk that knows the
-// ray's best root B so far (the non-flat part of the scene resolved first)
-// need only reach t = B + far_m / |d|: a sphere the reference accepts at a
+// The far cut (the render's walks run before its scan and do
+// not use it, t_stop = inf). A walk that knows the ray's best root B so far
+// (the non-flat part of the scene resolved first) need only reach t = B + far_m / |d|: a sphere the reference accepts at a
 // root c <= B has a point of its rho-ball chord at t <= c + e, e the fp32
 // root's error, <= 2 sqrt(8u) |o - c_i| / |d| (the discriminant's rounding,
 // 8u (hb^2 + a|cc|), through the square root) — far_m = 4e-3 (|o|max +
@@ -227,35 +220,6 @@ inline bool build_layer_grid(const float *sph, uint32_t i_lo, uint32_t i_hi, Lay
     G.nblk = (m + 7) / 8;
     cell.assign((size_t)G.nx * G.nz, 0ull);
     for (const auto &h : hits) cell[h.first] |= 1ull << (h.second / 8);
-    return true;
-}
-
-// Host: the block-list grid (large scenes): m spheres sph[4 j], sphere j in
-// block blk[j] (< 0xfffe); per cell kGridListSlots block ids (kGridNone: an
-// empty slot; kGridFull in slot 0: the cell names more blocks than it holds,
-// a walk through it scans every block).
-inline bool build_layer_grid_blocks(const float *sph, const uint32_t *blk, uint32_t m, uint32_t max_cells,
-                                    LayerGrid &G, std::vector<uint16_t> &slots) {
-    std::vector<std::pair<uint32_t, uint32_t>> hits;
-    if (!build_layer_grid_cells(sph, m, max_cells, G, [&](uint32_t k, uint32_t j) { hits.emplace_back(k, j); }))
-        return false;
-    uint32_t nb = 0;
-    for (uint32_t j = 0; j < m; ++j) nb = std::max(nb, blk[j] + 1u);
-    if (nb >= kGridFull) return false;
-    G.nblk = nb;
-    slots.assign((size_t)G.nx * G.nz * kGridListSlots, kGridNone);
-    for (const auto &h : hits) {
-        uint16_t *s = &slots[(size_t)h.first * kGridListSlots];
-        const uint16_t b = (uint16_t)blk[h.second];
-        if (s[0] == kGridFull) continue;
-        uint32_t q = 0;
-        while (q < kGridListSlots && s[q] != kGridNone && s[q] != b) ++q;
-        if (q == kGridListSlots) {
-            s[0] = kGridFull;  // overflow
-            continue;
-        }
-        s[q] = b;
-    }
     return true;
 }
 

@@ -62,12 +62,6 @@ struct KScene {
     // then per cell the mask of the run's blocks it may need (NULL: none,
     // every block is scanned)
     const LayerGrid *grid;
-    // block-list grid of the culled layout's flat section (large scenes;
-    // rtx_grid.h): its LayerGrid, then kGridListSlots u16 block ids (relative
-    // to cflat_lo) per cell (NULL: none); cgrid_ws: LDS words per wave of the
-    // walk's union (counter, overflow, bitmap over the section's blocks, list)
-    const LayerGrid *cgrid;
-    uint32_t cgrid_ws;
 };
 
 #ifndef RTX_CULL  // A/B build: 0 = no culled layout (the large-scene lane-mode scan visits every block)

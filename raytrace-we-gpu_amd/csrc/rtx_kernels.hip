@@ -743,17 +743,12 @@ __device__ __forceinline__ bool resolve_pre(const float4 *__restrict__ cen, uint
 // group is tested again, its earlier blocks masked off). Wave-uniform.
 // A bound also fails when it is wholly behind the lane's origin (the half
 // test H, Hs: rtx_prefilter.h HalfTest; 5 more fp32 ops per bound, 4 flat).
-// `end` (a multiple of 512 blocks, or the layout's end): the scan stops there.
-// `wl` (the grid's union of the wave's walks, wn flat-section blocks relative
-// to cflat_lo, GridWs): the scan visits those blocks instead of the hierarchy,
-// b then being the list position to resume at.
-__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, uint32_t end, const LineTest &T,
-                                                const LineTest &Ts, const HalfTest &H, const HalfTest &Hs,
-                                                uint32_t *list, uint32_t &cnt, const uint16_t *wl = nullptr,
-                                                uint32_t wn = 0u) {
+__device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, const LineTest &T, const LineTest &Ts,
+                                                const HalfTest &H, const HalfTest &Hs, uint32_t *list,
+                                                uint32_t &cnt) {
     cnt = 0;
     uint32_t *my = list + threadIdx.x;
-    const uint32_t nblk = min(S.n_cpad / 8u, end);
+    const uint32_t nblk = S.n_cpad / 8u;
     const LineFlat K = line_test_flat(T, S.flat_cy);
     // flat bounds: the ray stretched along y (rtx_prefilter.h kCullSy), the 5-op test
     const LineFlat Ks = line_test_flat(Ts, kCullSy * S.flat_cy);
@@ -893,20 +888,13 @@ __device__ __forceinline__ uint32_t scan_culled(const KScene &S, uint32_t b, uin
     // stretched) iff b0 >= cflat_lo (cflat_lo is a multiple of 512 blocks, so
     // no test straddles it: rtx_api.hip build_cull)
     auto bound_mask = [&](cfloat_p grp, uint32_t b0) -> uint32_t { return bound_mask1(grp, b0 >= S.cflat_lo); };
-    if (wl != nullptr) {  // the grid's blocks (all in the flat section), in list order
-        for (; b < wn; ++b) {
-            const uint32_t bb = S.cflat_lo + (uint32_t)__builtin_amdgcn_readfirstlane((int)wl[b]);
-            if (step(Flat(), bb)) return b + 1u;
-        }
-        return wn;
-    }
     // Three levels above the blocks: a group bound covers the 64 spheres of 8
     // blocks, a super bound the 512 of 8 groups; the super bounds are tested 8
     // at a time (4,096 spheres), then, for each passing super-group, its 8
     // group bounds, for each passing group its 8 block bounds, then the
     // passing blocks' spheres. A resumed scan (b inside a range) masks off
     // the super-groups, groups and blocks before b.
-    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u, nhg = (nsg + 7u) / 8u;  // (nblk: the end)
+    const uint32_t ng = (nblk + 7u) / 8u, nsg = (ng + 7u) / 8u, nhg = (nsg + 7u) / 8u;
     for (uint32_t hg = b >> 9; hg < nhg; ++hg) {
         uint32_t m3 = first_bits(nsg - 8u * hg);
         if (RTX_CULL_LEVELS >= 3) m3 &= bound_mask((cfloat_p)S.cbnd3 + 32u * hg, 512u * hg);
@@ -950,77 +938,8 @@ __device__ __forceinline__ HalfTest half_test_stretched(f3 o, f3 d, float thr_bs
     const float as = fmaf(d.z, d.z, fmaf(dys, dys, d.x * d.x));
     return half_test_setup(o.x, kCullSy * o.y, o.z, d.x, dys, d.z, as, thr_bs, t_min);
 }
-// The block-list grid of a large scene's flat layer (rtx_grid.h; DESIGN.md
-// §3f). Each wave keeps an LDS workspace (KScene::cgrid_ws words): [0] the
-// list's length, [1] spare, [2, 2 + bw) a bitmap over the flat section's
-// blocks, then the list (kGridListCap u16 block ids). grid_union: every lane
-// that reaches hit_world walks its ray's slab stretch (the far cut at its best
-// root so far: the non-flat part of the scene is resolved first), and each
-// block its cells name is set in the bitmap and, the first time, appended to
-// the list (LDS atomics). Returns the list's length, or ~0u when some lane
-// gave up (an unsafe ray, too long a walk, a full cell) or the list
-// overflowed: the wave then takes the culled scan over the whole section.
-__device__ __forceinline__ uint32_t grid_union(const KScene &S, uint32_t *ws, f3 o, f3 d, float a, float best,
-                                               bool safe) {
-    const LayerGrid G = *S.cgrid;  // wave-uniform: scalar loads
-    const uint2 *cells = reinterpret_cast<const uint2 *>(S.cgrid + 1);  // kGridListSlots u16 per cell
-    uint32_t *bmp = ws + 2;
-    uint16_t *lst = reinterpret_cast<uint16_t *>(ws + 2 + (G.nblk + 31u) / 32u);
-    auto mark = [&](uint32_t b) {
-        const uint32_t bit = 1u << (b & 31u);
-        const uint32_t old = __hip_atomic_fetch_or(bmp + (b >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((old & bit) == 0u) {
-            const uint32_t i = __hip_atomic_fetch_add(ws, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (i < kGridListCap) lst[i] = (uint16_t)b;
-        }
-    };
-    const float ts = fmaf(G.far_m, __builtin_amdgcn_rsqf(a), best);  // the far cut (+inf: none yet)
-    const bool ok = safe && grid_walk(G, kGridMaxStepsLarge, o.x, o.y, o.z, d.x, d.y, d.z, ts, [&](uint32_t k) {
-                        const uint2 c = cells[k];
-                        if ((c.x & 0xffffu) == kGridFull) return false;
-                        const uint32_t q[4] = {c.x & 0xffffu, c.x >> 16, c.y & 0xffffu, c.y >> 16};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (q[j] != kGridNone) mark(q[j]);
-                        return true;
-                    });
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    return (__ballot(!ok) != 0ull || n > kGridListCap) ? ~0u : n;
-}
-// After the scan: the bitmap back to zero (the listed blocks' words, or every
-// word after an overflow) and the length to 0, by the wave's active lanes.
-__device__ __forceinline__ void grid_clear(const KScene &S, uint32_t *ws) {
-    const uint32_t bw = (S.cgrid_ws - 2u - kGridListCap / 2u);
-    uint32_t *bmp = ws + 2;
-    const uint16_t *lst = reinterpret_cast<const uint16_t *>(ws + 2 + bw);
-    const uint64_t ex = __ballot(1);
-    const uint32_t na = (uint32_t)__popcll(ex);
-    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u));
-    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[0]);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (n <= kGridListCap) {
-        for (uint32_t j = r; j < n; j += na) bmp[lst[j] >> 5] = 0u;
-    } else {
-        for (uint32_t j = r; j < bw; j += na) bmp[j] = 0u;
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (r == 0u) ws[0] = 0u;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-// Zero every wave's workspace (all threads of the block; the caller synchronises).
-__device__ __forceinline__ void grid_ws_zero(const KScene &S, uint32_t *ws0, uint32_t nthreads) {
-    for (uint32_t i = threadIdx.x; i < (nthreads / 64u) * S.cgrid_ws; i += nthreads) ws0[i] = 0u;
-}
-
-// kGrid (its own kernel instances: the grid's code costs the plain culled
-// kernels registers they spill, R10e): gws is the wave's block-list grid
-// workspace (NULL or a scene without the grid: the culled scan over the
-// whole layout).
-template <bool kGrid = false>
 __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, float a, float inv_a, float t_min,
-                                                float &best, uint32_t *list, uint32_t *gws = nullptr) {
+                                                float &best, uint32_t *list) {
     const LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
     const LineTest Ts = line_test_stretched(S, o, d);
     const HalfTest H = half_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, T.thr * kCullThrScale, t_min);
@@ -1031,35 +950,14 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
     const uint32_t nblk = S.n_cpad / 8u;
     auto ld = [&S](uint32_t p) { return S.ccen[p]; };
     auto gi = [&S](uint32_t p) { return S.cperm[p]; };
-    auto resolve = [&](uint32_t cnt) {
+    uint32_t b = 0;
+    do {
+        uint32_t cnt;
+        b = scan_culled(S, b, T, Ts, H, Hs, list, cnt);
         ok = resolve_pre_t<decltype(ld), decltype(gi), true>(ld, S.n_cpad, list, cnt, o, d, a, inv_a, t_min, best,
                                                               idx, cand_of<true>(), gi) &&
              ok;
-    };
-    // the grid (RTX_GRID): the non-flat part first, the flat section by the wave's walks
-    const bool grid = kGrid && RTX_GRID && gws != nullptr && S.cgrid != nullptr && S.cflat_lo < nblk;
-    const uint32_t end1 = grid ? S.cflat_lo : nblk;
-    uint32_t b = 0;
-    while (b < end1) {
-        uint32_t cnt;
-        b = scan_culled(S, b, end1, T, Ts, H, Hs, list, cnt);
-        resolve(cnt);
-    }
-    if constexpr (kGrid) {
-      if (grid) {
-        const uint32_t wn = grid_union(S, gws, o, d, a, best, T.thr != -__uint_as_float(0x7f800000u));
-        const uint16_t *wl = reinterpret_cast<const uint16_t *>(gws + S.cgrid_ws - kGridListCap / 2u);
-        uint32_t k = wn == ~0u ? S.cflat_lo : 0u;
-        const uint32_t kend = wn == ~0u ? nblk : wn;
-        while (k < kend) {
-            uint32_t cnt;
-            k = wn == ~0u ? scan_culled(S, k, nblk, T, Ts, H, Hs, list, cnt)
-                          : scan_culled(S, k, nblk, T, Ts, H, Hs, list, cnt, wl, wn);
-            resolve(cnt);
-        }
-        grid_clear(S, gws);
-      }
-    }
+    } while (b < nblk);
     if (!ok) {
         RTX_DIAG_ADD(3, (uint32_t)__popcll(__ballot(1)));
         best = best0;
@@ -2198,13 +2096,9 @@ __device__ __forceinline__ void take_heavy(const KParams &P, const Frame &F, Hea
 // material fetch are then as cheap as in a whole-wave-only kernel (a
 // runtime lg cost the one-pixel-per-wave case 2.0 -> 2.5 us per segment,
 // profiles/R6f_pixel_timeline_r8.jsonl).
-// glist (a wave's LDS for the layer grid: 64 bytes per group; NULL: none):
-// the group scans only its ray's blocks — the blocks outside the scene's flat
-// run and the flat-run blocks its slab walk marks (rtx_grid.h grid_mask) —
-// listed in index order, 4 sphere pairs per block (scenes of up to 64 blocks).
 template <uint32_t kLg, typename Src>
 __device__ __forceinline__ void trace_group_segment(const KParams &P, const Frame &F, const Src &src, Lane &W,
-                                                    bool &ended, uint8_t *glist = nullptr) {
+                                                    bool &ended) {
     constexpr uint32_t lg = kLg;
     const KScene &S = P.scene;
     const uint32_t lane = threadIdx.x & 63u;
@@ -2214,38 +2108,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const int last = (int)S.n - 1;
     const ScatterSpec sp = scatter_spec(W.seed);
     LineTest T = line_test_setup(W.o.x, W.o.y, W.o.z, W.d.x, W.d.y, W.d.z, W.a, S.smag);
-    const bool idle = lg < 6u && !W.active;  // a group without a pixel: nothing is flagged (a whole wave is always active)
-    // the layer grid: this group's blocks, in order, into its glist (the walk is
-    // the same in every lane of the group: the same ray)
-    uint8_t *gl = glist ? glist + 64u * (lane >> lg) : nullptr;
-    uint32_t gcnt = 0;
-    if (gl != nullptr) {
-        const uint32_t nblk = S.n_pad / 8u;
-        const uint64_t all = nblk >= 64u ? ~0ull : (1ull << nblk) - 1ull;
-        const uint32_t fl = S.flat_hi - S.flat_lo;
-        const uint64_t run = (fl >= 64u ? ~0ull : (1ull << fl) - 1ull) << S.flat_lo;
-        uint64_t fm = 0ull;
-        if (!idle) {
-            const LayerGrid G = *S.grid;
-            const uint64_t *gc = reinterpret_cast<const uint64_t *>(S.grid + 1);
-            fm = T.thr == -inf ? ~0ull
-                               : grid_mask(G, [gc](uint32_t c) { return gc[c]; }, W.o.x, W.o.y, W.o.z, W.d.x, W.d.y,
-                                           W.d.z);
-        }
-        const uint64_t cm = idle ? 0ull : (all & ~run) | ((fm << S.flat_lo) & run);
-        constexpr uint32_t kBpl = 64u >> lg;  // bits per lane of the group
-#pragma unroll
-        for (uint32_t j = 0; j < kBpl; ++j) {
-            const uint32_t bit = k * kBpl + j;
-            if ((cm >> bit) & 1ull) gl[__popcll(cm & ((1ull << bit) - 1ull))] = (uint8_t)bit;
-        }
-        gcnt = (uint32_t)__popcll(cm);
-        // the lists are read by other lanes of the group: LDS keeps one wave's
-        // operations in order; the compiler must too
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-    }
-    if (idle) {
+    if (lg < 6u && !W.active) {  // a group without a pixel: nothing is flagged (a whole wave is always active)
         T.ux = T.uy = T.uz = T.vy = T.vz = T.nou = T.nov = 0.0f;
         T.thr = inf;
     }
@@ -2253,20 +2116,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
     const f2v nou = {T.nou, T.nou}, nov = {T.nov, T.nov}, th = {T.thr, T.thr};
     uint64_t key = hit_key(inf, -1);
     bool ok = true;
-    // the steps: every pair (SphLds: npairs is a multiple of 64), or, with the
-    // grid, the most any group of the wave needs (4 pairs per listed block)
-    const uint32_t npairs_g = 4u * gcnt;
-    const uint32_t nsteps = gl ? (group_reduce_u32<true>(npairs_g, 6u) + g - 1u) >> lg : src.npairs >> lg;
-    // step st's pair of this lane (valid: it has one)
-    auto pair_of = [&](uint32_t st, bool &valid) -> uint32_t {
-        if (gl == nullptr) {
-            valid = true;
-            return (st << lg) + k;
-        }
-        const uint32_t pos = (st << lg) + k;
-        valid = pos < npairs_g;
-        return valid ? 4u * (uint32_t)gl[pos >> 2] + (pos & 3u) : 0u;
-    };
+    const uint32_t nsteps = src.npairs >> lg;  // SphLds: npairs is a multiple of 64
 #pragma unroll 1
     for (uint32_t s0 = 0; s0 < nsteps; s0 += kGfSteps) {
         // the group coop's scan and resolve (hit_world_groups)
@@ -2274,12 +2124,10 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
         const uint32_t s1 = min(s0 + kGfSteps, nsteps);
         auto step = [&](uint32_t st) {
             f2v cx, cy, cz, R;
-            bool valid;
-            src.pair(pair_of(st, valid), cx, cy, cz, R);
+            src.pair((st << lg) + k, cx, cy, cz, R);
             const f2v pu = fma2(cx, ux, fma2(cy, uy, fma2(cz, uz, nou)));
             const f2v pv = fma2(cy, vy, fma2(cz, vz, nov));
-            f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
-            if (!valid) q = f2v{-inf, -inf};  // no pair: not flagged
+            const f2v q = fma2(-pv, pv, fma2(-pu, pu, R)) - th;
             im = (im << 1) | (__float_as_uint(q.y) >> 31);
             im = (im << 1) | (__float_as_uint(q.x) >> 31);
         };
@@ -2296,8 +2144,7 @@ __device__ __forceinline__ void trace_group_segment(const KParams &P, const Fram
             const bool live = fm != 0u;
             const uint32_t bit = live ? (uint32_t)__builtin_ctz(fm) : 0u;
             fm &= fm - 1u;
-            bool valid;
-            const uint32_t p = pair_of(s1 - 1u - (bit >> 1), valid);
+            const uint32_t p = ((s1 - 1u - (bit >> 1)) << lg) + k;
             const uint32_t j = 2u * p + (bit & 1u);
             resolve_one(src.sphere(j), (int)j, live, W.o, W.d, W.a, W.inv_a, kTMin, key, ok);
         }
@@ -2578,10 +2425,9 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
-template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false, bool kGrid = false>
+template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false>
 __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
-    constexpr bool kCGrid = kCulled && kGrid;            // ... with the block-list layer grid
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][coop LDS copy of the spheres]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     uint32_t *list = reinterpret_cast<uint32_t *>(s_mem);
@@ -2595,10 +2441,6 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
     const float *pf_tile = kPF && (RTX_PF_LDS || RTX_PF_RING) ? reinterpret_cast<const float *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
-    // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
-    uint32_t *gws0 = kCGrid && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + 16) : nullptr;
-    uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
-    if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     // promotion: the block's first wave to go idle serves the queue, the others leave
     __shared__ uint32_t s_server;
     const bool prom_on = kPersist && !kCost && P.prom != nullptr;
@@ -2725,7 +2567,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
         if (kCulled) {  // large scenes: the culled scan (block bounds first, scan_culled)
             if (L.active) {
                 float best = __uint_as_float(0x7f800000u);
-                const int hit = hit_world_culled<kCGrid>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws);
+                const int hit = hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
                 D.section(1);
                 promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
             }
@@ -2874,16 +2716,9 @@ __device__ __forceinline__ int take_promoted_groups(const KParams &P, const Fram
 // copy, took LDS the render's blocks needed: at R = 8 (7 k_trace waves per
 // CU) only ~79 % of k_render's lanes were resident (profiles/R6r_pixel_timelines.jsonl).
 constexpr uint32_t kTraceThreads = 256;
-constexpr uint32_t kTraceGlistBytes = 8u * 64u;  // per wave: 8 groups' block lists (trace_group_segment)
-__host__ __device__ constexpr uint32_t trace_glist_off(uint32_t n) { return (coop_lds_bytes(n) + 15u) & ~15u; }
 __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem), true, kTraceThreads);
-    // the layer grid's per-group block lists (64 bytes per group, 8 groups per
-    // wave at most), after the scene copy (trace_group_segment)
-    uint8_t *glist = P.scene.grid && P.scene.n_pad <= 512u
-                         ? s_mem + trace_glist_off(P.scene.n) + (threadIdx.x / 64u) * kTraceGlistBytes
-                         : nullptr;
     __syncthreads();
     const Frame F = load_frame(P);
     const uint32_t npix = P.rows_local * P.width;
@@ -2959,7 +2794,7 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
             // is this pixel's critical path)
             uint32_t n = 0;
             do {
-                trace_group_segment<6>(P, F, sl, W, ended, glist);
+                trace_group_segment<6>(P, F, sl, W, ended);
                 ++n;
                 if (P.prom) beat(P, last_beat);
             } while (!ended);
@@ -2967,11 +2802,11 @@ __global__ void __launch_bounds__(kTraceThreads, 4) k_trace(const KParams P) {
         } else {
             if (P.prom) beat(P, last_beat);
             if (lg == 5u)  // wave-uniform; trace_group 1, 2, 4 or 8 (rtx_set_schedule)
-                trace_group_segment<5>(P, F, sl, W, ended, glist);
+                trace_group_segment<5>(P, F, sl, W, ended);
             else if (lg == 4u)
-                trace_group_segment<4>(P, F, sl, W, ended, glist);
+                trace_group_segment<4>(P, F, sl, W, ended);
             else  // 8 pixels per wave, 8 lanes each: a third of the issue per pixel-segment of 16-lane groups
-                trace_group_segment<3>(P, F, sl, W, ended, glist);
+                trace_group_segment<3>(P, F, sl, W, ended);
             if (W.active && first) segs++;
         }
         if (ended) {
@@ -3243,10 +3078,9 @@ __device__ __forceinline__ void ps_fold(const KParams &P, uint32_t px0, uint32_t
     output_pixel(P, px0 + po, acc);
 }
 
-template <bool kPF, bool kLin = false, bool kGrid = false>
+template <bool kPF, bool kLin = false>
 __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
-    constexpr bool kCGrid = kCulled && kGrid;            // ... with the block-list layer grid
     // dynamic LDS: [candidate list, list_bytes<kPF>][coop rays, kCoopBytes][batch slots, kPsStateBytes]
     //              [LDS copy of the spheres (n <= kCoopLds)]
     extern __shared__ __attribute__((aligned(16))) unsigned char s_mem[];
@@ -3257,11 +3091,6 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
     uint32_t *st = reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) + (threadIdx.x / 64) * kPsSlots * 4;
     const bool sph_lds = !kPF && P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes + kPsStateBytes), sph_lds);
-    // the block-list grid's per-wave workspace (culled large scenes with a grid; grid_union)
-    uint32_t *gws0 = kCGrid && P.scene.cgrid ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes + kPsStateBytes)
-                                             : nullptr;
-    uint32_t *gws = gws0 ? gws0 + (threadIdx.x / 64u) * P.scene.cgrid_ws : nullptr;
-    if (gws0) grid_ws_zero(P.scene, gws0, kRB);
     const SphGlobal sg = sph_global(P.scene);
     const uint32_t lane = threadIdx.x & 63u;
     if (lane < kPsSlots * 4) st[lane] = 0u;
@@ -3334,7 +3163,7 @@ __global__ void RTX_PS_BOUNDS_T(kPF) k_render_ps(const KParams P) {
                 hit = hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
             }
         } else if (L.active) {  // (the SGPR scan: the LDS tile measured slower here)
-            hit = kCulled ? hit_world_culled<kCGrid>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, gws)
+            hit = kCulled ? hit_world_culled(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list)
                   : sph_lds ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d, L.a,
                                                     L.inv_a, kTMin, best, list)
                             : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list);
@@ -3447,12 +3276,6 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
                                                             float t_max, uint32_t start, float *out) {
     __shared__ uint32_t list[list_bytes<true>() > kListBytes ? list_bytes<true>() / sizeof(uint32_t)
                                                              : kListBytes / sizeof(uint32_t)];
-    // the block-list grid's per-wave workspace (dynamic: KScene::cgrid_ws words per wave)
-    extern __shared__ __attribute__((aligned(16))) uint32_t d_gws[];
-    if (S.cgrid) {
-        grid_ws_zero(S, d_gws, kRB);
-        __syncthreads();
-    }
     const uint32_t i = blockIdx.x * kRB + threadIdx.x;
     if (i >= nrays) return;
     const f3 o = mk3(rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]);
@@ -3462,8 +3285,7 @@ __global__ void __launch_bounds__(kRB) k_debug_hit_world(const KScene S, const f
     float best = t_max;
     const int idx =
         min((start == kDebugCulled && S.cpre)
-                ? hit_world_culled<true>(S, o, d, a, inv_a, t_min, best, list,
-                                         S.cgrid ? d_gws + (threadIdx.x / 64u) * S.cgrid_ws : nullptr)
+                ? hit_world_culled(S, o, d, a, inv_a, t_min, best, list)
             : S.n_pad > kScanPfMin ? hit_world_pre<true>(S, o, d, a, inv_a, t_min, best, list, nullptr, start)
                                    : hit_world_pre<false>(S, o, d, a, inv_a, t_min, best, list, nullptr, start),
             (int)S.n - 1);
@@ -3625,14 +3447,11 @@ static bool use_pf(const KScene &s) { return s.n_pad > kScanPfMin; }
 // every block of every segment (the reference's Hittable_list order of work,
 // with the prefilter), through the per-wave LDS tile in the chain render.
 static bool use_lin(const KScene &s) { return use_pf(s) && s.cpre == nullptr; }
-// the block-list layer grid (culled large scenes uploaded with one): its own instances
-static bool use_cgrid(const KScene &s) { return use_pf(s) && s.cpre != nullptr && s.cgrid != nullptr; }
 template <bool kPersist, bool kCost>
 static const void *render_fn(const KScene &s) {
-    return !use_pf(s)     ? (const void *)k_render<kPersist, kCost, false>
-           : use_lin(s)   ? (const void *)k_render<kPersist, kCost, true, true>
-           : use_cgrid(s) ? (const void *)k_render<kPersist, kCost, true, false, true>
-                          : (const void *)k_render<kPersist, kCost, true>;
+    return !use_pf(s)   ? (const void *)k_render<kPersist, kCost, false>
+           : use_lin(s) ? (const void *)k_render<kPersist, kCost, true, true>
+                        : (const void *)k_render<kPersist, kCost, true>;
 }
 template <bool kPersist, bool kCost>
 static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t stream, const KParams &a) {
@@ -3640,8 +3459,6 @@ static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((k_render<kPersist, kCost, false>), dim3(blocks), dim3(kRB), lds, stream, a);
     else if (use_lin(s))
         hipLaunchKernelGGL((k_render<kPersist, kCost, true, true>), dim3(blocks), dim3(kRB), lds, stream, a);
-    else if (use_cgrid(s))
-        hipLaunchKernelGGL((k_render<kPersist, kCost, true, false, true>), dim3(blocks), dim3(kRB), lds, stream, a);
     else
         hipLaunchKernelGGL((k_render<kPersist, kCost, true>), dim3(blocks), dim3(kRB), lds, stream, a);
 }
@@ -3650,8 +3467,7 @@ static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t s
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() + 16 + (use_lin(s) ? kPfLdsBytes : 0u) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
-           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0) +
-           (use_pf(s) && s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0);  // the grid's workspaces
+           (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 
 hipError_t launch_cost(const KParams &p, hipStream_t stream) {
@@ -3676,14 +3492,12 @@ constexpr uint32_t kPsItems = RTX_PS_ITEMS;
 constexpr uint32_t kPsBatchesPerWave = RTX_PS_BPW;
 static size_t ps_lds(const KScene &s) {
     return (use_pf(s) ? list_bytes<true>() : kListBytes) + kCoopBytes + kPsStateBytes +
-           (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0) +
-           (use_pf(s) && s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0);  // the grid's workspaces
+           (!use_pf(s) && s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }
 static const void *ps_fn(const KScene &s) {
-    return !use_pf(s)     ? (const void *)k_render_ps<false>
-           : use_lin(s)   ? (const void *)k_render_ps<true, true>
-           : use_cgrid(s) ? (const void *)k_render_ps<true, false, true>
-                          : (const void *)k_render_ps<true>;
+    return !use_pf(s)   ? (const void *)k_render_ps<false>
+           : use_lin(s) ? (const void *)k_render_ps<true, true>
+                        : (const void *)k_render_ps<true>;
 }
 static uint32_t ps_cap_of(uint32_t spp) { return max(kPsItems, spp); }
 // Every resident wave (an item is a sample, not a pixel: a frame share with
@@ -3718,8 +3532,6 @@ static hipError_t launch_ps(const KParams &p, const KSchedule &sched, hipStream_
         hipLaunchKernelGGL(k_render_ps<false>, dim3(blocks), dim3(kRB), lds, stream, q);
     else if (use_lin(p.scene))
         hipLaunchKernelGGL((k_render_ps<true, true>), dim3(blocks), dim3(kRB), lds, stream, q);
-    else if (use_cgrid(p.scene))
-        hipLaunchKernelGGL((k_render_ps<true, false, true>), dim3(blocks), dim3(kRB), lds, stream, q);
     else
         hipLaunchKernelGGL(k_render_ps<true>, dim3(blocks), dim3(kRB), lds, stream, q);
     return hipGetLastError();
@@ -3865,7 +3677,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     if (trace_waves > 0) {
         q.trace_ext = 1u;
         q.trace_lg = 6u - (uint32_t)__builtin_ctz(max(1u, min(tune.trace_group, 64u)));
-        const size_t tlds = trace_glist_off(p.scene.n) + (kTraceThreads / 64u) * kTraceGlistBytes;
+        const size_t tlds = coop_lds_bytes(p.scene.n);
         e = hipEventRecord(sched.ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(sched.aux, sched.ev_fork, 0);
         if (e != hipSuccess) return e;
@@ -3912,8 +3724,7 @@ hipError_t launch_debug_hit_world(const KScene &s, const float *rays, uint32_t n
                                s, rays, nrays, t_min, t_max, q, out);
         return hipGetLastError();
     }
-    const size_t glds = s.cgrid ? (size_t)(kRB / 64) * s.cgrid_ws * sizeof(uint32_t) : 0;
-    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), glds, stream, s,
+    hipLaunchKernelGGL(k_debug_hit_world, dim3(ceil_div(nrays, kRB)), dim3(kRB), 0, stream, s,
                        rays, nrays, t_min, t_max, start_block, out);
     return hipGetLastError();
 }

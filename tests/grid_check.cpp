@@ -60,9 +60,8 @@ static bool ref_accepts(const float o[3], const float d[3], const float *c, floa
 
 struct Layer {
     std::vector<float> s;  // (cx, cy, cz, r)
-    rtx::LayerGrid G, Gb;
+    rtx::LayerGrid G;
     std::vector<unsigned long long> cell;
-    std::vector<uint16_t> slots;  // the block-list grid of the same layer (blocks j / 8)
 };
 
 static bool make_layer(Layer &L, bool rtiow) {
@@ -82,33 +81,14 @@ static bool make_layer(Layer &L, bool rtiow) {
         for (int i = 0; i < n; ++i)
             L.s.insert(L.s.end(), {(float)(ext * sym()), y0, (float)(ext * sym()), (float)(rmax * (0.05 + 0.95 * uni()))});
     }
-    const uint32_t n = (uint32_t)(L.s.size() / 4);
-    std::vector<uint32_t> blk(n);
-    for (uint32_t j = 0; j < n; ++j) blk[j] = j / 8;
-    return rtx::build_layer_grid(L.s.data(), 0u, n, L.G, L.cell) &&
-           rtx::build_layer_grid_blocks(L.s.data(), blk.data(), n, 1u << 20, L.Gb, L.slots);
-}
-
-// The block-list grid's walk as the kernel runs it: the blocks of the cells
-// visited (as a 64-bit mask here: blocks j / 8 < 64), ~0 when it gives up or
-// meets a full cell.
-static uint64_t list_mask(const Layer &L, const float o[3], const float d[3], float t_stop) {
-    uint64_t m = 0ull;
-    const bool done = rtx::grid_walk(L.Gb, 4096u, o[0], o[1], o[2], d[0], d[1], d[2], t_stop, [&](uint32_t k) {
-        const uint16_t *s = &L.slots[(size_t)k * rtx::kGridListSlots];
-        if (s[0] == rtx::kGridFull) return false;
-        for (uint32_t q = 0; q < rtx::kGridListSlots; ++q)
-            if (s[q] != rtx::kGridNone) m |= 1ull << s[q];
-        return true;
-    });
-    return done ? m : ~0ull;
+    return rtx::build_layer_grid(L.s.data(), 0u, (uint32_t)(L.s.size() / 4), L.G, L.cell);
 }
 
 int main(int argc, char **argv) {
     const long nlayers = argc > 1 ? atol(argv[1]) : 300;
     const long nrays = argc > 2 ? atol(argv[2]) : 4000;
     long rays = 0, applied = 0, all = 0, accepted = 0, missed = 0, layers = 0, nogrid = 0;
-    long far_checked = 0, far_missed = 0, list_all = 0, list_missed = 0;
+    long far_checked = 0, far_missed = 0;
     double far_bits = 0.0;
     double bits = 0.0;
     for (long li = 0; li < nlayers; ++li) {
@@ -176,8 +156,6 @@ int main(int argc, char **argv) {
             bits += (double)__builtin_popcountll(m);
             std::vector<float> roots(n, INFINITY);
             float win = INFINITY;
-            const uint64_t ml = list_mask(L, of, df, INFINITY);
-            if (ml == ~0ull) ++list_all;
             for (uint32_t i = 0; i < n; ++i) {
                 const float *ci = &L.s[4 * (size_t)i];
                 const bool a0 = ref_accepts(of, df, ci, a, 0.0f);
@@ -192,7 +170,6 @@ int main(int argc, char **argv) {
                                 ci[0], ci[1], ci[2], ci[3], of[0], of[1], of[2], df[0], df[1], df[2]);
                     ++missed;
                 }
-                if (!((ml >> (i / 8)) & 1ull)) ++list_missed;
             }
             // the far cut (t_min 1e-3, the render's): B at the winner's own root
             // (a tie goes to the later sphere: every root <= B must be scanned),
@@ -203,13 +180,11 @@ int main(int argc, char **argv) {
                     const float B = rep == 0 ? win : win * (float)(0.5 + uni());
                     const float ts = fmaf(L.G.far_m, inv_len, B);
                     const uint64_t mf = rtx::grid_mask(L.G, cellf, of[0], of[1], of[2], df[0], df[1], df[2], ts);
-                    const uint64_t mlf = list_mask(L, of, df, fmaf(L.Gb.far_m, inv_len, B));
                     far_bits += (double)__builtin_popcountll(mf);
                     for (uint32_t i = 0; i < n; ++i) {
                         if (!(roots[i] <= B)) continue;
                         ++far_checked;
-                        const bool hit_m = (mf >> (i / 8)) & 1ull, hit_l = (mlf >> (i / 8)) & 1ull;
-                        if (!hit_m || !hit_l) {
+                        if (!((mf >> (i / 8)) & 1ull)) {
                             if (far_missed < 5)
                                 fprintf(stderr, "far miss: sphere %u root %.9g B %.9g o (%.9g %.9g %.9g) d (%.9g %.9g %.9g)\n",
                                         i, roots[i], B, of[0], of[1], of[2], df[0], df[1], df[2]);
@@ -223,8 +198,8 @@ int main(int argc, char **argv) {
     const long masked = applied - all;
     printf("{\"layers\": %ld, \"layers_without_grid\": %ld, \"rays\": %ld, \"grid_applied\": %ld, "
            "\"every_block\": %ld, \"accepted_spheres\": %ld, \"missed\": %ld, \"mean_blocks_marked\": %.3f, "
-           "\"far_checked\": %ld, \"far_missed\": %ld, \"list_every_block\": %ld, \"list_missed\": %ld}\n",
+           "\"far_checked\": %ld, \"far_missed\": %ld}\n",
            layers, nogrid, rays, applied, all, accepted, missed, masked ? bits / (double)masked : 0.0, far_checked,
-           far_missed, list_all, list_missed);
-    return missed == 0 && far_missed == 0 && list_missed == 0 ? 0 : 1;
+           far_missed);
+    return missed == 0 && far_missed == 0 ? 0 : 1;
 }

@@ -78,3 +78,16 @@ def test_gathered_parity_rows_cover_every_rank(bench, rtx):
         owners = {(r // T) % R for r in rows}
         assert owners == set(range(R)) and len(rows) == 2 * R and rows == sorted(rows)
         assert all(0 <= r < H for r in rows)
+
+
+def test_kernel_class_names_every_render_instance(bench):
+    """The PMC passes attribute counters by rocprof kernel name: every
+    k_render template instance (3 to 5 bool parameters) must map to its role,
+    or the bench line loses its executed-FLOP and issue fields."""
+    for n in (3, 4, 5):
+        rest = ", ".join(["false"] * (n - 1))
+        assert bench.kernel_class(f"void rtx::k_render<true, {rest}>(rtx::KParams)") == "render"
+        assert bench.kernel_class(f"void rtx::k_render<false, {rest}>(rtx::KParams)") == "render_grid"
+        assert bench.kernel_class(f"void rtx::k_render<false, true, {', '.join(['true'] * (n - 2))}>(x)") == "prepass"
+    assert bench.kernel_class("void rtx::k_render_ps<true, false, false>(rtx::KParams)") == "k_render_ps"
+    assert bench.kernel_class("__amd_rocclr_fillBufferAligned") is None

@@ -71,11 +71,8 @@ def test_layer_grid_never_skips_an_accepted_sphere(tmp_path):
     assert rep["accepted_spheres"] > 3_000_000 and rep["grid_applied"] > 900_000, rep
     assert rep["every_block"] < 0.01 * rep["grid_applied"], rep  # the walk rarely gives up
     # the far cut (the walk stops far_m / |d| past the best root so far: the
-    # winner's own root, ties included) and the block-list grid (large scenes)
+    # winner's own root, ties included)
     assert rep["far_missed"] == 0 and rep["far_checked"] > 500_000, rep
-    # (the random layers pack up to 512 spheres into few cells: a cell past
-    # kGridListSlots blocks is full and a walk through it scans every block)
-    assert rep["list_missed"] == 0 and rep["list_every_block"] < 0.35 * rep["grid_applied"], rep
     # sensitivity: the same checker over a grid without the margins misses
     bad = tmp_path / "bad" / "raytrace-we-gpu_amd" / "csrc"
     bad.mkdir(parents=True)
