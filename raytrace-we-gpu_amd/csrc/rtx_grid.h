@@ -63,7 +63,13 @@ namespace rtx {
 constexpr float kGridOMax = 64.0f;      // rays with |o| above this scan every block
 constexpr double kGridFatCells = 1.0 / 256.0;  // cell-list fattening, in cells
 constexpr double kGridSlabPad = 1e-3;          // slab half-width past rho_max (y units)
-constexpr uint32_t kGridMaxSteps = 48;  // a longer walk scans every block
+#ifndef RTX_GRID_STEPS  // A/B: the walk's step limit
+#define RTX_GRID_STEPS 48
+#endif
+#ifndef RTX_GRID_HLOG  // A/B: cell side 2^k times the one-sphere-per-cell size
+#define RTX_GRID_HLOG 0
+#endif
+constexpr uint32_t kGridMaxSteps = RTX_GRID_STEPS;  // a longer walk scans every block
 constexpr uint32_t kGridMaxCells = 4096;  // cells of a grid at most
 
 struct LayerGrid {
@@ -175,7 +181,7 @@ inline bool build_layer_grid_cells(const float *sph, uint32_t m, uint32_t max_ce
     }
     // cell side: the power of two nearest one sphere per cell, at least rho_max
     const double area = std::fmax((xhi - xlo) * (zhi - zlo), 1e-30);
-    double h = std::exp2(std::round(std::log2(std::sqrt(area / m))));
+    double h = std::exp2(std::round(std::log2(std::sqrt(area / m))) + RTX_GRID_HLOG);
     while (h < rho_max) h *= 2.0;
     const double fat = kGridFatCells * h;
     // the box: a spare cell on every side (no disc reaches it)
