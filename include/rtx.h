@@ -38,8 +38,10 @@ extern "C" {
 #define RTX_API
 #endif
 
-#define RTX_VERSION 144 /* 1.4.4 */
+#define RTX_VERSION 145 /* 1.4.5 */
 /* ABI notes.
+ *  1.4.5: schedule defaults tier1_bar_low 2.0 -> 1.8 and promote_low 300 ->
+ *         500 (the R = 4 share with the layer grid, S6k-S6l; no layout change).
  *  1.4.4: rtx_set_scan_mode (RTX_SCAN_AUTO / RTX_SCAN_LINEAR; a new entry
  *         point, no layout change).
  *  1.4.3: RTX_DEBUG_CULLED_COOP_LANE(q) (the culled coop's per-lane walk);
@@ -236,7 +238,7 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
 typedef struct rtx_schedule {
     float tier1_bar;          /* default 1.7 */
     float tier1_bar_small;    /* default 1.6 */
-    float tier1_bar_low;      /* default 2.0 */
+    float tier1_bar_low;      /* default 1.8 (2.0 before 1.4.5) */
     float tier2_bar_small;    /* default 2.0 */
     float tier2_bar_medium;   /* default 1e30 (none; 1.2 in earlier builds) */
     float tier2_bar;          /* default 1e30 (no tier 2 for a larger part) */
@@ -252,7 +254,7 @@ typedef struct rtx_schedule {
     float trace_medium;       /* default 0.15 */
     float trace_large;        /* default 0 */
     float promote_small;      /* default 400; each promote_* in [0, 1e9] */
-    float promote_low;        /* default 300 */
+    float promote_low;        /* default 500 (300 before 1.4.5) */
     float promote_medium;     /* default 400 */
     float promote_large;      /* default 400 */
     float promote_big_scene;  /* default 60: every part of a scene above 640 spheres */

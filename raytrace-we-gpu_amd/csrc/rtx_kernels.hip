@@ -127,7 +127,7 @@ constexpr double kHeavyAlpha = 2.0;     // tier 2 (small share) iff key > alpha 
 constexpr double kHeavy1Alpha = 1.7;    // tier 1 iff key > alpha1 * share
 constexpr double kHeavy1AlphaSmall = 1.6;   // the same for a small frame share (2.5 until round 4, 4.0 until R4b)
 constexpr double kHeavyRhoLow = 2.5;        // "low" share: fewer pixels than this * resident lanes
-constexpr double kHeavy1AlphaLow = 2.0;     // tier-1 bar for a low share (3.0 until round 4, 3.5 until R4b)
+constexpr double kHeavy1AlphaLow = 1.8;     // tier-1 bar for a low share (2.0 until S6l, 3.0 until round 4, 3.5 until R4b)
 constexpr double kHeavyRho = 1.2;       // "small" frame share: fewer pixels than rho * resident lanes
 constexpr double kHeavyRho2 = 3.5;      // "medium" frame share: fewer pixels than rho2 * resident lanes
 // tier 2 for a medium share: key > this * share (default: none). 1.2 until round 4 (2-way split 37 -> 34 ms
@@ -146,7 +146,7 @@ constexpr double kTraceSmall = 0.35, kTraceLow = 0.3, kTraceMedium = 0.15, kTrac
 // 30.6-31.1 -> 29.6-30.0 ms at 250-500; 4- and 8-way splits: with k_trace's
 // pixel groups serving the queue, 300-400 (150: 40 ms at R = 8, the queue
 // floods; profiles/R6j_*)
-constexpr double kPromSmall = 400.0, kPromLow = 300.0, kPromMedium = 400.0, kPromLarge = 400.0;
+constexpr double kPromSmall = 400.0, kPromLow = 500.0, kPromMedium = 400.0, kPromLarge = 400.0;  // low: 300 until S6l
 // scenes without the coop's LDS copy (C5: 100k spheres, a lane-mode segment ~2 ms for the heaviest
 // pixels): any part, C5 1,827 -> 1,638 ms at 60 (150: 1,734, 25: 1,657; profiles/R4b_c5_promL.jsonl)
 constexpr double kPromBig = 60.0;

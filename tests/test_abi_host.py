@@ -50,7 +50,7 @@ def test_library_built_for_gfx950(rtx):
 
 def test_version_and_error_paths(rtx):
     lib = rtx.load_library()
-    assert lib.rtx_version() == 144
+    assert lib.rtx_version() == 145
     # null arguments are rejected without touching the GPU
     assert lib.rtx_upload_world(None, None) == -1
     assert b"null" in lib.rtx_last_error()
@@ -104,7 +104,7 @@ def test_schedule_defaults_and_validation(rtx):
     field before a context exists (a null ctx is refused first)."""
     d = rtx.schedule_defaults()
     assert d.tier1_bar == pytest.approx(1.7) and d.tier1_bar_small == pytest.approx(1.6)
-    assert d.tier1_bar_low == pytest.approx(2.0) and d.tier2_bar_small == pytest.approx(2.0)
+    assert d.tier1_bar_low == pytest.approx(1.8) and d.tier2_bar_small == pytest.approx(2.0)
     assert d.tier2_bar_medium == pytest.approx(1e30) and d.small_share == pytest.approx(1.2)
     assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
     assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 32 and d.tail_coop_max_large == 8
@@ -112,7 +112,7 @@ def test_schedule_defaults_and_validation(rtx):
     assert d.tier2_bar == pytest.approx(1e30)
     assert (d.tier1_priority, d.tier2_priority, d.hot_priority) == (3, 2, 3)
     assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == pytest.approx((0.35, 0.3, 0.15, 0.0))
-    assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (400.0, 300.0, 400.0, 400.0)
+    assert (d.promote_small, d.promote_low, d.promote_medium, d.promote_large) == (400.0, 500.0, 400.0, 400.0)
     assert d.promote_big_scene == 60.0
     assert (d.trace_group, d.trace_solo_bar, d.prepass_cap_split) == (4, pytest.approx(6.0), 0)
     assert (d.prio_bar1, d.prio_bar2, d.prio_bar3) == pytest.approx((0.5, 1.0, 1.5))
