@@ -479,8 +479,9 @@ def test_c5_full_width_rows(gpu_ctx, oracle, rtx):
     """C5 at full size (BASELINE configs[4]: 100k spheres, 1920x1080, spp 16,
     depth 50) on the bench's schedule: the kPF scan with its pack start,
     lane mode with 24-entry lists, the 1-spp persistent pre-pass, the tail
-    coop reading the scene from HBM. Two full 1920-px rows bit-exact against
-    the oracle; the frame's segment count (the scheduled render's own
+    coop reading the scene from HBM. Eight full 1920-px rows spread over the
+    image (sky, horizon, the far and near field, the big spheres) bit-exact
+    against the oracle; the frame's segment count (the scheduled render's own
     counter) equal to the per-pixel counts of an independent exact-grid pass
     (rtx_debug_pixel_cost), whose sums over those rows equal the oracle's."""
     W, H = 1920, 1080
@@ -488,7 +489,7 @@ def test_c5_full_width_rows(gpu_ctx, oracle, rtx):
     frame = rtx.camera_look_at(W, H)
     img, st = render_gpu(gpu_ctx, world, frame)
     assert st.samples == W * H * 16
-    rows = np.array([317, 771], np.uint32)
+    rows = np.unique(np.concatenate([np.linspace(4, H - 5, 6), [317, 771]])).astype(np.uint32)
     want, segs = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
     assert_bits_equal(img[rows], want, "C5 rows")
     assert np.isfinite(img).all()
@@ -502,9 +503,9 @@ def test_per_sample_c5_full_width_rows(gpu_ctx, oracle, rtx):
     spheres, spp 16, depth 50) — the path where round 3's illegal-address
     fault hit ("Faults"): k_render_ps with the kPF SGPR scan
     (no per-wave LDS tile in this kernel) and its group-coop tail reading the
-    scene from HBM. Two full rows bit-exact against the oracle in the same
-    RNG mode; the frame's segment count equal to an independent exact-grid
-    pass's per-pixel counts (rtx_debug_pixel_cost, per-sample seeds too),
+    scene from HBM. Eight full rows (spread over the image) bit-exact against
+    the oracle in the same RNG mode; the frame's segment count equal to an
+    independent exact-grid pass's per-pixel counts (rtx_debug_pixel_cost, per-sample seeds too),
     whose sums over those rows equal the oracle's."""
     W, H = 1920, 1080
     world = rtx.random_world(159, capacity=100000, depth=50, spp=16)
@@ -512,7 +513,7 @@ def test_per_sample_c5_full_width_rows(gpu_ctx, oracle, rtx):
     frame.rng_mode = 1
     img, st = render_gpu(gpu_ctx, world, frame)
     assert st.samples == W * H * 16
-    rows = np.array([211, 866], np.uint32)
+    rows = np.unique(np.concatenate([np.linspace(9, H - 9, 6), [211, 866]])).astype(np.uint32)
     want, segs = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
     assert_bits_equal(img[rows], want, "per-sample C5 rows")
     assert np.isfinite(img).all()
