@@ -2852,17 +2852,35 @@ __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, u
     return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
 }
 constexpr uint32_t kSortPerThread = 16;
+// The sort's enumeration of the pixels: row-major (RTX_QUEUE_TILE 0), or
+// tile-major in T x T tiles (a bucket then lists a tile's pixels together, so
+// a wave's run of consecutive slots comes from a compact patch of the image).
+// j in [0, sort_span) -> pixel index, or ~0u for a slot of a partial tile.
+#ifndef RTX_QUEUE_TILE
+#define RTX_QUEUE_TILE 0
+#endif
+__host__ __device__ __forceinline__ uint32_t sort_span(uint32_t width, uint32_t rows) {
+    if (RTX_QUEUE_TILE == 0) return width * rows;
+    const uint32_t T = RTX_QUEUE_TILE;
+    return ((width + T - 1) / T) * ((rows + T - 1) / T) * T * T;
+}
+__device__ __forceinline__ uint32_t sort_pixel(uint32_t j, uint32_t width, uint32_t rows) {
+    if (RTX_QUEUE_TILE == 0) return j < width * rows ? j : ~0u;
+    const uint32_t T = RTX_QUEUE_TILE, tx = (width + T - 1) / T;
+    const uint32_t t = j / (T * T), u = j % (T * T);
+    const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * T + u / T;
+    return (x < width && y < rows) ? y * width + x : ~0u;
+}
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                       uint32_t cost_spp, uint32_t sat_cap, uint32_t *counts) {
     __shared__ uint32_t h[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
-    const uint32_t n = width * rows;
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
+        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        if (i != ~0u) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock)
@@ -2881,12 +2899,11 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
-    const uint32_t n = width * rows;
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = base + k * kBlock + threadIdx.x;
-        key[k] = i < n ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
-        rank[k] = i < n ? atomicAdd(&h[key[k]], 1u) : 0u;
+        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        key[k] = i != ~0u ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
+        rank[k] = i != ~0u ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2901,8 +2918,8 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) {
+        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        if (i != ~0u) {
             const uint32_t g = start[key[k]] + rank[k];
             perm[g] = i;
             if (inv) inv[i] = g;  // coalesced: pixel i's queue slot (k_unpermute)
@@ -3608,7 +3625,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         launch_k<false, true>(p.scene, need, lds, stream, c);
     }
     // 2. counting sort by cost, descending
-    const uint32_t sblocks = ceil_div(lanes, kBlock * kSortPerThread);
+    const uint32_t sblocks = ceil_div(sort_span(p.width, p.rows_local), kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                        p.rows_local, c.spp, split_cap, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
