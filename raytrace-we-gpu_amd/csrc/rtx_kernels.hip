@@ -2425,6 +2425,27 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
+// Tile-major enumerations of a W x rows pixel grid: j in [0, tile_span) ->
+// pixel index (row-major within a T x T tile, tiles row-major), or ~0u for a
+// slot of a partial tile; T = 0: row-major, the identity. The exact-grid
+// render (RTX_EXACT_TILE: a wave's 64 lanes an 8 x 8 patch) and the cost
+// sort (RTX_QUEUE_TILE, below) use them: spatially close rays share more of
+// the layer grid's and the culled scan's blocks.
+__host__ __device__ __forceinline__ uint32_t tile_span(uint32_t width, uint32_t rows, uint32_t T) {
+    return T == 0u ? width * rows : ((width + T - 1u) / T) * ((rows + T - 1u) / T) * T * T;
+}
+__device__ __forceinline__ uint32_t tile_pixel(uint32_t j, uint32_t width, uint32_t rows, uint32_t T) {
+    if (T == 0u) return j < width * rows ? j : ~0u;
+    const uint32_t tx = (width + T - 1u) / T;
+    const uint32_t t = j / (T * T), u = j % (T * T);
+    const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * T + u / T;
+    return (x < width && y < rows) ? y * width + x : ~0u;
+}
+#ifndef RTX_EXACT_TILE
+#define RTX_EXACT_TILE 0
+#endif
+constexpr uint32_t kExactTile = RTX_EXACT_TILE;
+
 template <bool kPersist, bool kCost = false, bool kPF = false, bool kLin = false>
 __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     constexpr bool kCulled = kPF && RTX_CULL && !kLin;  // the culled scan (large scenes, not the linear mode)
@@ -2464,7 +2485,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     L.cb = L.ce = 0u;
     bool exhausted = !kPersist;
     if (!kPersist) {
-        const uint32_t gid = blockIdx.x * kRB + threadIdx.x;
+        const uint32_t gid = tile_pixel(blockIdx.x * kRB + threadIdx.x, P.width, P.rows_local, kExactTile);
         if (gid < npix) start_pixel(P, F, gid, L);
     }
     // heavy slots [0, kh) of the queue (k_heavy_split; tier 1 = [0, k1)), normal slots [kh, npix)
@@ -2856,9 +2877,13 @@ constexpr uint32_t kSortPerThread = 16;
 // tile-major in T x T tiles (a bucket then lists a tile's pixels together, so
 // a wave's run of consecutive slots comes from a compact patch of the image).
 // j in [0, sort_span) -> pixel index, or ~0u for a slot of a partial tile.
-#ifndef RTX_QUEUE_TILE
-#define RTX_QUEUE_TILE 0
+#ifndef RTX_QUEUE_TILE  // 16: C2 37.7 -> 35.8 ms with the layer grid (S6q-S6r); 0 = row-major
+#define RTX_QUEUE_TILE 16
 #endif
+#ifndef RTX_QUEUE_MORTON
+#define RTX_QUEUE_MORTON 0
+#endif
+static_assert(!RTX_QUEUE_MORTON || (RTX_QUEUE_TILE & (RTX_QUEUE_TILE - 1)) == 0, "Morton tiles: a power of two");
 __host__ __device__ __forceinline__ uint32_t sort_span(uint32_t width, uint32_t rows) {
     if (RTX_QUEUE_TILE == 0) return width * rows;
     const uint32_t T = RTX_QUEUE_TILE;
@@ -2868,7 +2893,16 @@ __device__ __forceinline__ uint32_t sort_pixel(uint32_t j, uint32_t width, uint3
     if (RTX_QUEUE_TILE == 0) return j < width * rows ? j : ~0u;
     const uint32_t T = RTX_QUEUE_TILE, tx = (width + T - 1) / T;
     const uint32_t t = j / (T * T), u = j % (T * T);
+#if RTX_QUEUE_MORTON  // Morton order inside the tile (T a power of two)
+    uint32_t ux = 0, uy = 0;
+    for (uint32_t b = 0; (1u << b) < T; ++b) {
+        ux |= ((u >> (2 * b)) & 1u) << b;
+        uy |= ((u >> (2 * b + 1)) & 1u) << b;
+    }
+    const uint32_t x = (t % tx) * T + ux, y = (t / tx) * T + uy;
+#else
     const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * T + u / T;
+#endif
     return (x < width && y < rows) ? y * width + x : ~0u;
 }
 
@@ -3493,7 +3527,7 @@ hipError_t launch_cost(const KParams &p, hipStream_t stream) {
     const size_t lds = render_lds(p.scene);
     hipError_t e = allow_lds(render_fn<false, true>(p.scene), lds);
     if (e != hipSuccess) return e;
-    launch_k<false, true>(p.scene, ceil_div(lanes, kRB), lds, stream, p);
+    launch_k<false, true>(p.scene, ceil_div(tile_span(p.width, p.rows_local, kExactTile), kRB), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -3565,6 +3599,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     const uint64_t lanes = (uint64_t)p.rows_local * p.width;
     if (lanes == 0) return hipSuccess;
     const uint32_t need = ceil_div(lanes, kRB);
+    const uint32_t need_x = ceil_div(tile_span(p.width, p.rows_local, kExactTile), kRB);  // the exact grid's blocks
     if (p.spp == 0 || p.depth == 0) {
         hipLaunchKernelGGL(k_render_trivial, dim3(ceil_div(lanes, kBlock)), dim3(kBlock), 0, stream, p);
         return hipGetLastError();
@@ -3578,7 +3613,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     if (e == hipSuccess) e = allow_lds(render_fn<true, true>(p.scene), lds);
     if (e != hipSuccess) return e;
     if (!sched.cost || p.spp < kLptMinSpp) {
-        launch_k<false, false>(p.scene, need, lds, stream, p);
+        launch_k<false, false>(p.scene, need_x, lds, stream, p);
         return hipGetLastError();
     }
     if (sched.nbuckets != kCostBuckets || sched.npix < lanes) return hipErrorInvalidValue;
@@ -3622,7 +3657,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         }
         launch_k<true, true>(p.scene, pblocks, lds, stream, c);
     } else {
-        launch_k<false, true>(p.scene, need, lds, stream, c);
+        launch_k<false, true>(p.scene, need_x, lds, stream, c);
     }
     // 2. counting sort by cost, descending
     const uint32_t sblocks = ceil_div(sort_span(p.width, p.rows_local), kBlock * kSortPerThread);
