@@ -2427,10 +2427,10 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
 // Tile-major enumerations of a W x rows pixel grid: j in [0, tile_span) ->
 // pixel index (row-major within a T x T tile, tiles row-major), or ~0u for a
-// slot of a partial tile; T = 0: row-major, the identity. The exact-grid
-// render (RTX_EXACT_TILE: a wave's 64 lanes an 8 x 8 patch) and the cost
-// sort (RTX_QUEUE_TILE, below) use them: spatially close rays share more of
-// the layer grid's and the culled scan's blocks.
+// slot of a partial tile; T = 0: row-major, the identity. The cost sort
+// uses them (RTX_QUEUE_TILE, below): spatially close rays share more of the
+// layer grid's blocks. The exact grid can too (RTX_EXACT_TILE 8: a wave's 64
+// lanes an 8 x 8 patch; an A/B option, flat at C2: S6s).
 __host__ __device__ __forceinline__ uint32_t tile_span(uint32_t width, uint32_t rows, uint32_t T) {
     return T == 0u ? width * rows : ((width + T - 1u) / T) * ((rows + T - 1u) / T) * T * T;
 }
@@ -2873,38 +2873,14 @@ __device__ __forceinline__ uint32_t cost_key(const uint32_t *cost, uint32_t i, u
     return (kCostBuckets - 1u) - min(sum, kCostBuckets - 1u);  // bucket 0 = most expensive
 }
 constexpr uint32_t kSortPerThread = 16;
-// The sort's enumeration of the pixels: row-major (RTX_QUEUE_TILE 0), or
-// tile-major in T x T tiles (a bucket then lists a tile's pixels together, so
-// a wave's run of consecutive slots comes from a compact patch of the image).
-// j in [0, sort_span) -> pixel index, or ~0u for a slot of a partial tile.
-#ifndef RTX_QUEUE_TILE  // 16: C2 37.7 -> 35.8 ms with the layer grid (S6q-S6r); 0 = row-major
+// The sort enumerates the pixels tile by tile (tile_pixel, RTX_QUEUE_TILE x
+// RTX_QUEUE_TILE tiles; 0: row-major): a bucket then lists a tile's pixels
+// together, so a wave's run of consecutive slots comes from a compact patch
+// of the image (C2 37.7 -> 35.8 ms with the layer grid).
+#ifndef RTX_QUEUE_TILE
 #define RTX_QUEUE_TILE 16
 #endif
-#ifndef RTX_QUEUE_MORTON
-#define RTX_QUEUE_MORTON 0
-#endif
-static_assert(!RTX_QUEUE_MORTON || (RTX_QUEUE_TILE & (RTX_QUEUE_TILE - 1)) == 0, "Morton tiles: a power of two");
-__host__ __device__ __forceinline__ uint32_t sort_span(uint32_t width, uint32_t rows) {
-    if (RTX_QUEUE_TILE == 0) return width * rows;
-    const uint32_t T = RTX_QUEUE_TILE;
-    return ((width + T - 1) / T) * ((rows + T - 1) / T) * T * T;
-}
-__device__ __forceinline__ uint32_t sort_pixel(uint32_t j, uint32_t width, uint32_t rows) {
-    if (RTX_QUEUE_TILE == 0) return j < width * rows ? j : ~0u;
-    const uint32_t T = RTX_QUEUE_TILE, tx = (width + T - 1) / T;
-    const uint32_t t = j / (T * T), u = j % (T * T);
-#if RTX_QUEUE_MORTON  // Morton order inside the tile (T a power of two)
-    uint32_t ux = 0, uy = 0;
-    for (uint32_t b = 0; (1u << b) < T; ++b) {
-        ux |= ((u >> (2 * b)) & 1u) << b;
-        uy |= ((u >> (2 * b + 1)) & 1u) << b;
-    }
-    const uint32_t x = (t % tx) * T + ux, y = (t / tx) * T + uy;
-#else
-    const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * T + u / T;
-#endif
-    return (x < width && y < rows) ? y * width + x : ~0u;
-}
+constexpr uint32_t kQueueTile = RTX_QUEUE_TILE;
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                       uint32_t cost_spp, uint32_t sat_cap, uint32_t *counts) {
@@ -2913,7 +2889,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
     __syncthreads();
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
         if (i != ~0u) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
     }
     __syncthreads();
@@ -2922,9 +2898,9 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 }
 
 // Positions: bucket start (prefix of the global counts) + a range the
-// block reserves in the bucket + the element's rank inside the block. The
-// order within a bucket is arbitrary; per-pixel results do not depend on it.
-// (Tile-major order within a bucket measured no faster: DESIGN.md §7.)
+// block reserves in the bucket + the element's rank inside the block: the
+// enumeration's order (tile-major) within a bucket, blocks in any order.
+// Per-pixel results do not depend on it.
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          uint32_t cost_spp, uint32_t sat_cap,
                                                          const uint32_t *counts, uint32_t *cursors,
@@ -2935,7 +2911,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
         key[k] = i != ~0u ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
         rank[k] = i != ~0u ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
@@ -2952,7 +2928,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = sort_pixel(base + k * kBlock + threadIdx.x, width, rows);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
         if (i != ~0u) {
             const uint32_t g = start[key[k]] + rank[k];
             perm[g] = i;
@@ -3660,7 +3636,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         launch_k<false, true>(p.scene, need_x, lds, stream, c);
     }
     // 2. counting sort by cost, descending
-    const uint32_t sblocks = ceil_div(sort_span(p.width, p.rows_local), kBlock * kSortPerThread);
+    const uint32_t sblocks = ceil_div(tile_span(p.width, p.rows_local, kQueueTile), kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
                        p.rows_local, c.spp, split_cap, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
