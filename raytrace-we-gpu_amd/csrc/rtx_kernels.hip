@@ -3671,7 +3671,12 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // 4, 8 shares measured no better, profiles/R3x_parts.jsonl)
     // and small scenes only (at 100k spheres a pixel takes ~100 ms in lane
     // mode, and heavy pixels waited in busy waves' runs: C5 1.88 -> 2.05 s)
-    q.chunk = !pf && (double)lanes / ((double)blocks * kRB) >= tune.rho2 ? min(tune.chunk, 4096u) : 0u;
+#ifndef RTX_CHUNK_ALL  // A/B: 1 = private runs for large scenes too, 2 = and for every share size
+#define RTX_CHUNK_ALL 0
+#endif
+    q.chunk = (RTX_CHUNK_ALL >= 2 || ((RTX_CHUNK_ALL >= 1 || !pf) && (double)lanes / ((double)blocks * kRB) >= tune.rho2))
+                  ? min(tune.chunk, 4096u)
+                  : 0u;
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     // tier 1 in k_trace on the auxiliary stream (small scenes): its waves
