@@ -40,8 +40,11 @@ extern "C" {
 
 #define RTX_VERSION 145 /* 1.4.5 */
 /* ABI notes.
- *  1.4.5: schedule defaults tier1_bar_low 2.0 -> 1.8 and promote_low 300 ->
- *         500 (the R = 4 share with the layer grid, S6k-S6l; no layout change).
+ *  1.4.5: schedule defaults tier1_bar_low 2.0 -> 1.8, promote_low 300 ->
+ *         500 (the R = 4 share with the layer grid, S6k-S6l) and
+ *         refill_chunk 16 -> 64 (the queue in pixel tiles, S6t-S6u); private
+ *         runs (at most 16 slots) also for large scenes and medium shares;
+ *         no layout change.
  *  1.4.4: rtx_set_scan_mode (RTX_SCAN_AUTO / RTX_SCAN_LINEAR; a new entry
  *         point, no layout change).
  *  1.4.3: RTX_DEBUG_CULLED_COOP_LANE(q) (the culled coop's per-lane walk);
@@ -220,8 +223,10 @@ RTX_API int rtx_use_own_stream(rtx_ctx *ctx);
  *     spheres (no LDS copy: a segment is a long scan there, so a far
  *     shorter remaining chain is worth handing to a whole wave);
  *   - refill_chunk: for a part of at least medium_share pixels per lane (a
- *     whole frame), each wave takes its pixels from a private run of this
- *     many consecutive slots of the cost-ordered queue, re-stocked when
+ *     whole frame) of a scene up to 1,024 spheres, each wave takes its pixels
+ *     from a private run of this many consecutive slots of the cost-ordered
+ *     queue (at most 16 for a larger scene or a part of low_share to
+ *     medium_share pixels per lane; none below), re-stocked when
  *     empty, so its lanes hold pixels from few runs (coherent rays) rather
  *     than one slot per refill from wherever the queue head is; the last
  *     eighth of the queue is taken slot by slot;
@@ -265,7 +270,7 @@ typedef struct rtx_schedule {
     uint32_t tier1_priority;  /* default 3 */
     uint32_t tier2_priority;  /* default 2 */
     uint32_t hot_priority;    /* default 3 */
-    uint32_t refill_chunk;    /* default 16; 0..4096 (0, 1: one refill per need) */
+    uint32_t refill_chunk;    /* default 64 (16 before 1.4.5); 0..4096 (0, 1: one refill per need) */
     uint32_t trace_group;     /* default 4: tier-1 pixels per wave of the tier-1 kernel (1, 2, 4 or 8; 8 since 1.4.1) */
     uint32_t prepass_cap_split; /* default 0 (none): a row-split part's cost pre-pass stops a pixel past this
                                    many segments (0..4096); it goes to the top of the queue (tier 1) and the

@@ -2881,6 +2881,7 @@ constexpr uint32_t kSortPerThread = 16;
 #define RTX_QUEUE_TILE 16
 #endif
 constexpr uint32_t kQueueTile = RTX_QUEUE_TILE;
+constexpr uint32_t kChunkShare = 16;  // the private runs of large scenes and medium shares (launch_render)
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                       uint32_t cost_spp, uint32_t sat_cap, uint32_t *counts) {
@@ -2968,7 +2969,7 @@ KTune default_tune() {
     t.prio_t1 = 3;
     t.prio_t2 = 2;
     t.prio_hot = 3;
-    t.chunk = 16;  // C2 45.9 -> 44.5 ms, 12-16 best (profiles/R3w_*, R3x_*)
+    t.chunk = 64;  // C2 35.9 -> 33.0 ms with the queue tiles (16 until S6u: 45.9 -> 44.5 ms then, R3w_*, R3x_*)
     t.trace_small = kTraceSmall;
     t.trace_low = kTraceLow;
     t.trace_medium = kTraceMedium;
@@ -3671,12 +3672,17 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     // 4, 8 shares measured no better, profiles/R3x_parts.jsonl)
     // and small scenes only (at 100k spheres a pixel takes ~100 ms in lane
     // mode, and heavy pixels waited in busy waves' runs: C5 1.88 -> 2.05 s)
-#ifndef RTX_CHUNK_ALL  // A/B: 1 = private runs for large scenes too, 2 = and for every share size
-#define RTX_CHUNK_ALL 0
-#endif
-    q.chunk = (RTX_CHUNK_ALL >= 2 || ((RTX_CHUNK_ALL >= 1 || !pf) && (double)lanes / ((double)blocks * kRB) >= tune.rho2))
-                  ? min(tune.chunk, 4096u)
-                  : 0u;
+    // private runs of the queue (refill): refill_chunk slots for a small
+    // scene's whole frame (C2 35.9 -> 33.0 ms at 64: S6t-S6u), at most
+    // kChunkShare for a large scene (C5 128.7 -> 124.4 ms at 16; 64: 140) and
+    // for a medium share (R = 2: 24.1 -> 22.4 ms at 16); none for smaller
+    // shares (R = 4: 16.1 -> 16.9 ms with them)
+    {
+        const double ppl = (double)lanes / ((double)blocks * kRB);
+        q.chunk = (!pf && ppl >= tune.rho2) ? min(tune.chunk, 4096u)
+                  : ppl >= tune.rho_low     ? min(tune.chunk, kChunkShare)
+                                            : 0u;
+    }
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     // tier 1 in k_trace on the auxiliary stream (small scenes): its waves

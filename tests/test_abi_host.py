@@ -108,7 +108,7 @@ def test_schedule_defaults_and_validation(rtx):
     assert d.tier2_bar_medium == pytest.approx(1e30) and d.small_share == pytest.approx(1.2)
     assert d.low_share == pytest.approx(2.5) and d.medium_share == pytest.approx(3.5)
     assert d.hot_fraction == pytest.approx(0.2) and d.tail_coop_max == 32 and d.tail_coop_max_large == 8
-    assert d.refill_chunk == 16
+    assert d.refill_chunk == 64
     assert d.tier2_bar == pytest.approx(1e30)
     assert (d.tier1_priority, d.tier2_priority, d.hot_priority) == (3, 2, 3)
     assert (d.trace_small, d.trace_low, d.trace_medium, d.trace_large) == pytest.approx((0.35, 0.3, 0.15, 0.0))
