@@ -2884,13 +2884,14 @@ constexpr uint32_t kQueueTile = RTX_QUEUE_TILE;
 constexpr uint32_t kChunkShare = 16;  // the private runs of large scenes and medium shares (launch_render)
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
-                                                      uint32_t cost_spp, uint32_t sat_cap, uint32_t *counts) {
+                                                      uint32_t cost_spp, uint32_t sat_cap, uint32_t tile,
+                                                      uint32_t *counts) {
     __shared__ uint32_t h[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
         if (i != ~0u) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
     }
     __syncthreads();
@@ -2903,7 +2904,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // enumeration's order (tile-major) within a bucket, blocks in any order.
 // Per-pixel results do not depend on it.
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
-                                                         uint32_t cost_spp, uint32_t sat_cap,
+                                                         uint32_t cost_spp, uint32_t sat_cap, uint32_t tile,
                                                          const uint32_t *counts, uint32_t *cursors,
                                                          uint32_t *perm, uint32_t *inv) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
@@ -2912,7 +2913,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
         key[k] = i != ~0u ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
         rank[k] = i != ~0u ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
@@ -2929,7 +2930,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, kQueueTile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
         if (i != ~0u) {
             const uint32_t g = start[key[k]] + rank[k];
             perm[g] = i;
@@ -3637,9 +3638,16 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
         launch_k<false, true>(p.scene, need_x, lds, stream, c);
     }
     // 2. counting sort by cost, descending
-    const uint32_t sblocks = ceil_div(tile_span(p.width, p.rows_local, kQueueTile), kBlock * kSortPerThread);
+    // (in pixel tiles except for a small share: R = 8 12.7 vs 13.0 ms, S6r, S6v)
+#ifndef RTX_QUEUE_TILE_ALL  // A/B: 1 = pixel tiles for every share size
+#define RTX_QUEUE_TILE_ALL 0
+#endif
+    const uint32_t qtile = RTX_QUEUE_TILE_ALL || (double)lanes >= tune.rho * (double)min(need, resident_blocks(render_fn<true, false>(p.scene), lds)) * kRB
+                               ? kQueueTile
+                               : 0u;
+    const uint32_t sblocks = ceil_div(tile_span(p.width, p.rows_local, qtile), kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, split_cap, sched.buckets);
+                       p.rows_local, c.spp, split_cap, qtile, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
     uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(p.scene), lds));
@@ -3652,7 +3660,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, p.spp,
                        heavy, tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, split_cap, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
+                       p.rows_local, c.spp, split_cap, qtile, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
                        sched.stage ? sched.inv : nullptr);
     KParams q = p;
     q.cost_spp = c.spp;
