@@ -2431,14 +2431,17 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // uses them (RTX_QUEUE_TILE, below): spatially close rays share more of the
 // layer grid's blocks. The exact grid can too (RTX_EXACT_TILE 8: a wave's 64
 // lanes an 8 x 8 patch; an A/B option, flat at C2: S6s).
-__host__ __device__ __forceinline__ uint32_t tile_span(uint32_t width, uint32_t rows, uint32_t T) {
-    return T == 0u ? width * rows : ((width + T - 1u) / T) * ((rows + T - 1u) / T) * T * T;
+__host__ __device__ __forceinline__ uint32_t tile_span(uint32_t width, uint32_t rows, uint32_t T, uint32_t TY = 0u) {
+    if (TY == 0u) TY = T;
+    return T == 0u ? width * rows : ((width + T - 1u) / T) * ((rows + TY - 1u) / TY) * T * TY;
 }
-__device__ __forceinline__ uint32_t tile_pixel(uint32_t j, uint32_t width, uint32_t rows, uint32_t T) {
+// (T x TY tiles; TY = 0: square)
+__device__ __forceinline__ uint32_t tile_pixel(uint32_t j, uint32_t width, uint32_t rows, uint32_t T, uint32_t TY = 0u) {
     if (T == 0u) return j < width * rows ? j : ~0u;
+    if (TY == 0u) TY = T;
     const uint32_t tx = (width + T - 1u) / T;
-    const uint32_t t = j / (T * T), u = j % (T * T);
-    const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * T + u / T;
+    const uint32_t t = j / (T * TY), u = j % (T * TY);
+    const uint32_t x = (t % tx) * T + u % T, y = (t / tx) * TY + u / T;
     return (x < width && y < rows) ? y * width + x : ~0u;
 }
 #ifndef RTX_EXACT_TILE
@@ -2885,13 +2888,13 @@ constexpr uint32_t kChunkShare = 16;  // the private runs of large scenes and me
 
 __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                       uint32_t cost_spp, uint32_t sat_cap, uint32_t tile,
-                                                      uint32_t *counts) {
+                                                      uint32_t tile_y, uint32_t *counts) {
     __shared__ uint32_t h[kCostBuckets];
     for (uint32_t b = threadIdx.x; b < kCostBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile, tile_y);
         if (i != ~0u) atomicAdd(&h[cost_key(cost, i, width, rows, cost_spp, sat_cap)], 1u);
     }
     __syncthreads();
@@ -2905,6 +2908,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_hist(const uint32_t *cost, uint
 // Per-pixel results do not depend on it.
 __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, uint32_t width, uint32_t rows,
                                                          uint32_t cost_spp, uint32_t sat_cap, uint32_t tile,
+                                                         uint32_t tile_y,
                                                          const uint32_t *counts, uint32_t *cursors,
                                                          uint32_t *perm, uint32_t *inv) {
     __shared__ uint32_t h[kCostBuckets], start[kCostBuckets];
@@ -2913,7 +2917,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
     const uint32_t base = blockIdx.x * kBlock * kSortPerThread;
     uint32_t rank[kSortPerThread], key[kSortPerThread];
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile, tile_y);
         key[k] = i != ~0u ? cost_key(cost, i, width, rows, cost_spp, sat_cap) : 0u;
         rank[k] = i != ~0u ? atomicAdd(&h[key[k]], 1u) : 0u;
     }
@@ -2930,7 +2934,7 @@ __global__ void __launch_bounds__(kBlock) k_cost_scatter(const uint32_t *cost, u
         if (h[b]) start[b] += atomicAdd(&cursors[b], h[b]);
     __syncthreads();
     for (uint32_t k = 0; k < kSortPerThread; ++k) {
-        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile);
+        const uint32_t i = tile_pixel(base + k * kBlock + threadIdx.x, width, rows, tile, tile_y);
         if (i != ~0u) {
             const uint32_t g = start[key[k]] + rank[k];
             perm[g] = i;
@@ -3642,12 +3646,18 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
 #ifndef RTX_QUEUE_TILE_ALL  // A/B: 1 = pixel tiles for every share size
 #define RTX_QUEUE_TILE_ALL 0
 #endif
-    const uint32_t qtile = RTX_QUEUE_TILE_ALL || (double)lanes >= tune.rho * (double)min(need, resident_blocks(render_fn<true, false>(p.scene), lds)) * kRB
-                               ? kQueueTile
-                               : 0u;
-    const uint32_t sblocks = ceil_div(tile_span(p.width, p.rows_local, qtile), kBlock * kSortPerThread);
+#ifndef RTX_QUEUE_TILE_SPLIT  // A/B: a row-split part's tiles, this wide and one row tile (tile_rows) tall
+#define RTX_QUEUE_TILE_SPLIT 0
+#endif
+    // a part's rows are runs of tile_rows image rows: its tiles are one run tall
+    uint32_t qtile = RTX_QUEUE_TILE_ALL || (double)lanes >= tune.rho * (double)min(need, resident_blocks(render_fn<true, false>(p.scene), lds)) * kRB
+                         ? kQueueTile
+                         : 0u;
+    uint32_t qtile_y = 0u;
+    if (RTX_QUEUE_TILE_SPLIT != 0 && p.nparts > 1u && p.tile_rows != 0u) qtile = RTX_QUEUE_TILE_SPLIT, qtile_y = p.tile_rows;
+    const uint32_t sblocks = ceil_div(tile_span(p.width, p.rows_local, qtile, qtile_y), kBlock * kSortPerThread);
     hipLaunchKernelGGL(k_cost_hist, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, split_cap, qtile, sched.buckets);
+                       p.rows_local, c.spp, split_cap, qtile, qtile_y, sched.buckets);
     // 3. heavy-pixel split (from the histogram), the ordered queue, then
     // the persistent render over it
     uint32_t blocks = min(need, resident_blocks(render_fn<true, false>(p.scene), lds));
@@ -3660,7 +3670,7 @@ hipError_t launch_render(const KParams &p_in, const KSchedule &sched, hipStream_
     hipLaunchKernelGGL(k_heavy_split, dim3(1), dim3(64), 0, stream, sched.buckets, (uint32_t)lanes, blocks * kRB, p.spp,
                        heavy, tune);
     hipLaunchKernelGGL(k_cost_scatter, dim3(sblocks), dim3(kBlock), 0, stream, sched.cost, p.width,
-                       p.rows_local, c.spp, split_cap, qtile, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
+                       p.rows_local, c.spp, split_cap, qtile, qtile_y, sched.buckets, sched.buckets + kCostBuckets, sched.perm,
                        sched.stage ? sched.inv : nullptr);
     KParams q = p;
     q.cost_spp = c.spp;
