@@ -500,7 +500,9 @@ def launch_desc(n_spheres, spp, nparts, rng, scan_mode="auto"):
         pre = ("k_render<false,true> 2-spp exact-grid cost pre-pass (samples 0-1, resumed from"
                + ("; a pixel past 16 segments stops and restarts in the render)" if whole else ")"))
     return (f"rtx_render_rows launch = {pre} + k_cost_hist + k_heavy_split + k_cost_scatter + "
-            f"k_render<true> (cost-ordered persistent lanes at a wave priority from their projected remaining "
+            f"k_render<true> (cost-ordered persistent lanes"
+            + (" — queue in 16x16 pixel tiles, 64-slot private runs per wave —" if whole and not large else "")
+            + f" at a wave priority from their projected remaining "
             f"chains, {scan}, heavy-pixel coop tiers, promotion)"
             + (" [+ k_trace on the aux stream for a row-split share]" if not large and not whole else ""))
 
