@@ -755,14 +755,9 @@ int rtx_upload_world(rtx_ctx *c, const rtx_world *w) {
     }
     if (has_grid) {
         static_assert(sizeof(rtx::LayerGrid) % 8 == 0, "the cells follow the LayerGrid, 8-byte aligned");
-        // [LayerGrid][u64 mask per cell][u32 compact word per cell, if every cell fits one]
-        std::vector<uint32_t> ccell;
-        grid.ncompact = rtx::compact_grid_cells(gcell, ccell) ? (uint32_t)ccell.size() : 0u;
-        std::vector<unsigned long long> buf(sizeof(rtx::LayerGrid) / 8 + gcell.size() + (ccell.size() + 1) / 2);
+        std::vector<unsigned long long> buf(sizeof(rtx::LayerGrid) / 8 + gcell.size());
         std::memcpy(buf.data(), &grid, sizeof grid);
         std::memcpy(buf.data() + sizeof(rtx::LayerGrid) / 8, gcell.data(), gcell.size() * sizeof(unsigned long long));
-        if (grid.ncompact)
-            std::memcpy(buf.data() + sizeof(rtx::LayerGrid) / 8 + gcell.size(), ccell.data(), ccell.size() * sizeof(uint32_t));
         RTX_HIP(hipMalloc(&c->d_grid, buf.size() * sizeof(unsigned long long)));
         RTX_HIP(hipMemcpyAsync(c->d_grid, buf.data(), buf.size() * sizeof(unsigned long long), hipMemcpyHostToDevice,
                                c->stream));

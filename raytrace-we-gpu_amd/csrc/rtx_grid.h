@@ -79,32 +79,7 @@ struct LayerGrid {
     uint32_t nx, nz;   // cells along x and z; cell (ix, iz) covers [x0 + ix h, x0 + (ix + 1) h] x ...
     float far_m;       // far cut: the walk may stop kGridFar(...) past the best root so far (distance units)
     uint32_t nblk;     // blocks the cells' masks name (<= 64)
-    uint32_t ncompact; // cells of the compact table after the masks (0: none; compact_grid_cells)
-    uint32_t pad_;
 };
-
-// The compact form of the cells' masks (one 32-bit word per cell, small
-// enough for the render's LDS): bits 0-7 the lowest block a cell names, bits
-// 8-23 the mask of blocks [lo, lo + 16) — the same set, when every cell's
-// blocks span fewer than 16 (the RTIOW layer: blocks of 8 spheres along z,
-// a cell's neighbours within a few blocks). Returns false (no compact table)
-// otherwise, or past max_cells cells.
-constexpr uint32_t kGridCompactMaxCells = 1024;  // 4 KiB: what the C2 render's LDS has left at 5 blocks per CU
-RTX_GD uint64_t grid_compact_mask(uint32_t v) { return (uint64_t)(v >> 8) << (v & 0xffu); }
-template <typename Vec>
-inline bool compact_grid_cells(const std::vector<unsigned long long> &cell, Vec &out) {
-    if (cell.size() > kGridCompactMaxCells) return false;
-    out.assign(cell.size(), 0u);
-    for (size_t k = 0; k < cell.size(); ++k) {
-        const uint64_t m = cell[k];
-        if (m == 0ull) continue;
-        const uint32_t lo = (uint32_t)__builtin_ctzll(m), hi = 63u - (uint32_t)__builtin_clzll(m);
-        if (hi - lo >= 16u) return false;
-        out[k] = lo | ((uint32_t)(m >> lo) << 8);
-        if (grid_compact_mask(out[k]) != m) return false;
-    }
-    return true;
-}
 
 // The far cut (the render's walks run before its scan and do
 // not use it, t_stop = inf). A walk that knows the ray's best root B so far

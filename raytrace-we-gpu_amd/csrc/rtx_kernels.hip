@@ -972,16 +972,11 @@ __device__ __forceinline__ int hit_world_culled(const KScene &S, f3 o, f3 d, flo
 // through one LDS word per wave, the list's spare row at the wave's first two
 // lanes (`spare`: the list's row `cap`, never a list entry). A lane outside
 // the prefilter's safe range marks every block.
-// gcc: the cells' compact words in the workgroup's LDS (k_render's copy,
-// grid_lds_ok), or NULL: the 64-bit masks from global memory.
-__device__ __forceinline__ uint64_t grid_wave_mask(const KScene &S, f3 o, f3 d, const LineTest &T, uint32_t *spare,
-                                                   const uint32_t *gcc = nullptr) {
+__device__ __forceinline__ uint64_t grid_wave_mask(const KScene &S, f3 o, f3 d, const LineTest &T, uint32_t *spare) {
     const LayerGrid G = *S.grid;  // wave-uniform: scalar loads
     const uint64_t *gc = reinterpret_cast<const uint64_t *>(S.grid + 1);
-    const uint64_t mine = T.thr == -__uint_as_float(0x7f800000u) ? ~0ull
-                          : gcc != nullptr
-                              ? grid_mask(G, [gcc](uint32_t k) { return grid_compact_mask(gcc[k]); }, o.x, o.y, o.z,
-                                          d.x, d.y, d.z)
+    const uint64_t mine = T.thr == -__uint_as_float(0x7f800000u)
+                              ? ~0ull
                               : grid_mask(G, [gc](uint32_t k) { return gc[k]; }, o.x, o.y, o.z, d.x, d.y, d.z);
     unsigned long long *w = reinterpret_cast<unsigned long long *>(spare + (threadIdx.x & ~63u));
     const uint32_t lead = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x);
@@ -1015,7 +1010,7 @@ template <bool kPF, typename Ld, bool kTile = false, bool kGridOk = true>
 __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3 d, float a, float inv_a,
                                                 float t_min, float &best, uint32_t *list, uint32_t *pack = nullptr,
                                                 uint32_t start = 0, const float *lds_pr = nullptr,
-                                                bool live = true, const uint32_t *gcc = nullptr) {
+                                                bool live = true) {
     const cfloat_p pre = (cfloat_p)S.pre;
     const uint32_t nblk = S.n_pad / 8;
     LineTest T = line_test_setup(o.x, o.y, o.z, d.x, d.y, d.z, a, S.smag);
@@ -1026,7 +1021,7 @@ __device__ __forceinline__ int hit_world_pre_ld(const KScene &S, Ld ld, f3 o, f3
     // the layer grid (small scenes, rtx_grid.h): the flat run's blocks some lane of the wave needs
     uint64_t gm = ~0ull;
     if constexpr (!kPF && kGridOk) {
-        if (RTX_GRID && S.grid != nullptr) gm = grid_wave_mask(S, o, d, T, list + cand_of<kPF>() * kRB, gcc);
+        if (RTX_GRID && S.grid != nullptr) gm = grid_wave_mask(S, o, d, T, list + cand_of<kPF>() * kRB);
     }
     const float best0 = best;
     int idx = -1;
@@ -2430,22 +2425,6 @@ __device__ __forceinline__ bool pre_stop(const KParams &P, uint32_t npix, Lane &
 // lanes pull pixels from the (cost-ordered) queue until it is exhausted;
 // otherwise an exact grid, one pixel per lane. kCost: the scheduling
 // pre-pass (P.cost_out: per-pixel segments, P.state: the state to resume).
-// The layer grid's compact cells in LDS (RTX_GRID_LDS): the small-scene
-// render kernels copy them after the spheres' LDS copy when the workgroup's
-// LDS still fits 5 workgroups per CU (kGridLdsBytes = kGridCompactMaxCells
-// words). The walk then reads a cell from LDS instead of L1/L2.
-#ifndef RTX_GRID_LDS
-#define RTX_GRID_LDS 1
-#endif
-constexpr uint32_t kGridLdsBytes = kGridCompactMaxCells * 4u;
-__host__ __device__ constexpr uint32_t grid_lds_off(uint32_t n) {
-    return (kListBytes + kCoopBytes + coop_lds_bytes(n) + 15u) & ~15u;
-}
-__host__ __device__ constexpr bool grid_lds_ok(uint32_t n) {
-    return n <= kCoopLds && grid_lds_off(n) + kGridLdsBytes <= 32768u;
-}
-static_assert(list_bytes<false>() == kListBytes, "grid_lds_off assumes the small-scene list size");
-
 // Tile-major enumerations of a W x rows pixel grid: j in [0, tile_span) ->
 // pixel index (row-major within a T x T tile, tiles row-major), or ~0u for a
 // slot of a partial tile; T = 0: row-major, the identity. The cost sort
@@ -2482,22 +2461,6 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
     // the coop's sphere data: a block-wide LDS copy for small scenes (SphLds)
     const bool coop_lds = P.scene.n <= kCoopLds;
     const SphLds sl = lds_copy(P.scene, reinterpret_cast<float *>(s_mem + kLB + kCoopBytes), coop_lds);
-    // the layer grid's compact cells, after the spheres' copy (render_lds
-    // reserves the room when grid_lds_ok; synchronised with the copy below)
-    const uint32_t *gcc = nullptr;
-    if constexpr (!kPF && !kLin) {
-        if (RTX_GRID_LDS && P.scene.grid != nullptr && coop_lds && grid_lds_ok(P.scene.n)) {
-            const LayerGrid *G = P.scene.grid;
-            const uint32_t nc = G->ncompact;  // wave-uniform: a scalar load
-            if (nc != 0u) {
-                uint32_t *dst = reinterpret_cast<uint32_t *>(s_mem + grid_lds_off(P.scene.n));
-                const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint64_t *>(G + 1) +
-                                                                         (size_t)G->nx * G->nz);
-                for (uint32_t i = threadIdx.x; i < nc; i += kRB) dst[i] = src[i];
-                gcc = dst;
-            }
-        }
-    }
     const SphGlobal sg = sph_global(P.scene);
     // kPF scenes never fit the LDS copy: its place holds the scan's pack word
     uint32_t *pack = kPF ? reinterpret_cast<uint32_t *>(s_mem + kLB + kCoopBytes) : nullptr;
@@ -2646,7 +2609,7 @@ __global__ void RTX_RENDER_BOUNDS_T2(kPF, kLin) k_render(const KParams P) {
             const int hit = (!kPF && coop_lds)  // kPF scenes (> kScanPfMin) never fit
                                 ? hit_world_pre_ld<kPF>(P.scene, [sl](uint32_t i) { return sl.sphere(i); }, L.o, L.d,
                                                         L.a, L.inv_a, kTMin, best, list, nullptr, 0,
-                                                        RTX_SCAN_LDS ? sl.pr : nullptr, true, gcc)
+                                                        RTX_SCAN_LDS ? sl.pr : nullptr)
                                 : hit_world_pre<kPF>(P.scene, L.o, L.d, L.a, L.inv_a, kTMin, best, list, pack);
             D.section(1);
             promoted = shade<kCost>(P, F, L, min(hit, last), best, prom_on && exhausted ? P.prom_min : 0u);
@@ -3536,8 +3499,6 @@ static void launch_k(const KScene &s, uint32_t blocks, size_t lds, hipStream_t s
 // Dynamic LDS of the chain-RNG kernels: candidate lists + coop ray slots +
 // the block's copy of the spheres for scenes up to kCoopLds.
 static size_t render_lds(const KScene &s) {
-    if (RTX_GRID_LDS && !use_pf(s) && s.grid != nullptr && grid_lds_ok(s.n))  // + the grid's compact cells
-        return grid_lds_off(s.n) + kGridLdsBytes;
     return (use_pf(s) ? list_bytes<true>() + 16 + (use_lin(s) ? kPfLdsBytes : 0u) : kListBytes) + kCoopBytes +  // kPF: the pack word (and the tile scan's tile)
            (s.n <= kCoopLds ? (size_t)coop_lds_bytes(s.n) : 0);
 }

@@ -88,7 +88,7 @@ int main(int argc, char **argv) {
     const long nlayers = argc > 1 ? atol(argv[1]) : 300;
     const long nrays = argc > 2 ? atol(argv[2]) : 4000;
     long rays = 0, applied = 0, all = 0, accepted = 0, missed = 0, layers = 0, nogrid = 0;
-    long far_checked = 0, far_missed = 0, compact_layers = 0, compact_bad = 0, rtiow_not_compact = 0;
+    long far_checked = 0, far_missed = 0;
     double far_bits = 0.0;
     double bits = 0.0;
     for (long li = 0; li < nlayers; ++li) {
@@ -98,17 +98,6 @@ int main(int argc, char **argv) {
             continue;
         }
         ++layers;
-        // the compact cell table (the render's LDS copy): when built, the same sets
-        {
-            std::vector<uint32_t> cc;
-            if (rtx::compact_grid_cells(L.cell, cc)) {
-                ++compact_layers;
-                for (size_t k = 0; k < cc.size(); ++k)
-                    if (rtx::grid_compact_mask(cc[k]) != L.cell[k]) ++compact_bad;
-            } else if (li % 3 == 0) {
-                ++rtiow_not_compact;
-            }
-        }
         const uint32_t n = (uint32_t)(L.s.size() / 4);
         const float y0 = L.s[1];
         auto cellf = [&L](uint32_t k) { return (uint64_t)L.cell[k]; };
@@ -209,9 +198,8 @@ int main(int argc, char **argv) {
     const long masked = applied - all;
     printf("{\"layers\": %ld, \"layers_without_grid\": %ld, \"rays\": %ld, \"grid_applied\": %ld, "
            "\"every_block\": %ld, \"accepted_spheres\": %ld, \"missed\": %ld, \"mean_blocks_marked\": %.3f, "
-           "\"far_checked\": %ld, \"far_missed\": %ld, \"compact_layers\": %ld, \"compact_bad\": %ld, "
-           "\"rtiow_not_compact\": %ld}\n",
+           "\"far_checked\": %ld, \"far_missed\": %ld}\n",
            layers, nogrid, rays, applied, all, accepted, missed, masked ? bits / (double)masked : 0.0, far_checked,
-           far_missed, compact_layers, compact_bad, rtiow_not_compact);
-    return missed == 0 && far_missed == 0 && compact_bad == 0 ? 0 : 1;
+           far_missed);
+    return missed == 0 && far_missed == 0 ? 0 : 1;
 }

@@ -73,9 +73,6 @@ def test_layer_grid_never_skips_an_accepted_sphere(tmp_path):
     # the far cut (the walk stops far_m / |d| past the best root so far: the
     # winner's own root, ties included)
     assert rep["far_missed"] == 0 and rep["far_checked"] > 500_000, rep
-    # the compact cell table the render copies to LDS: the same sets, and
-    # every RTIOW layer has one (a cell's blocks span fewer than 16)
-    assert rep["compact_bad"] == 0 and rep["rtiow_not_compact"] == 0 and rep["compact_layers"] >= 100, rep
     # sensitivity: the same checker over a grid without the margins misses
     bad = tmp_path / "bad" / "raytrace-we-gpu_amd" / "csrc"
     bad.mkdir(parents=True)
