@@ -694,6 +694,37 @@ def test_partitions_reassemble_bit_identical(gpu_ctx, rtx, nparts, tile_rows):
     image.free()
 
 
+def test_tiled_queue_whole_frame_equals_split(gpu_ctx, oracle, rtx):
+    """The cost queue's orders: a whole 1920x1080 frame
+    enumerates its queue in 16 x 16 pixel tiles with 64-slot private runs, a
+    2-way share in tiles with runs of 16, an 8-way share row by row without
+    runs. Every pixel's chain is its own, so all three must give the same
+    image: the whole frame equals both split frames reassembled, bit for bit
+    over every pixel (the frame's partial tiles at the bottom edge included),
+    with equal segment counts, and rows of it equal the oracle's."""
+    W, H, T = 1920, 1080, 5
+    world = rtx.random_world(11, depth=50, spp=12)
+    frame = rtx.camera_look_at(W, H, aspect=W / H)
+    full, st = render_gpu(gpu_ctx, world, frame)
+    for nparts in (2, 8):
+        max_rows = rtx.part_rows(H, T, 0, nparts)
+        gathered = gpu_ctx.alloc((nparts, max_rows, W, 4))
+        image = gpu_ctx.alloc((H, W, 4))
+        segs = 0
+        for p in range(nparts):
+            gpu_ctx.stats_reset()
+            gpu_ctx.render_rows(T, p, nparts, gathered.ptr + p * max_rows * W * 16)
+            segs += gpu_ctx.stats().segments
+        gpu_ctx.deinterleave(gathered.ptr, W, H, T, nparts, image.ptr)
+        assert_bits_equal(image.numpy(), full, f"whole frame vs {nparts} parts")
+        assert segs == st.segments
+        gathered.free()
+        image.free()
+    rows = np.array([0, 533, 1077, 1079], np.uint32)
+    want, _ = oracle.render_rows(world, frame, rows, nthreads=min(16, os.cpu_count() or 1))
+    assert_bits_equal(full[rows], want, "whole-frame rows")
+
+
 @pytest.mark.parametrize("nparts,part", [(8, 3), (4, 0), (2, 1)])
 def test_rank_share_of_c2_bit_exact(gpu_ctx, oracle, rtx, nparts, part):
     """One rank's share of the C2 frame (rtx_render_rows with R parts): a
